@@ -1,0 +1,134 @@
+/*
+ * dse.h -- C ABI of the MI355X dipolar spin-ensemble state-vector engine (libdse.so).
+ *
+ * The reference has no native boundary: its only solver entry is the Python call
+ *   simulate_rare(params) -> (t, obs)          dipolar_ensemble_with_rare.py:611-680
+ * which builds H with QuTiP (:453-588), prepares psi0 (:591-606) and hands both to
+ *   qt.sesolve(H, psi0, t, e_ops=[6 ops], options)   dipolar_ensemble_with_rare.py:653-666
+ * The functions below replace that sesolve call (and the operator algebra feeding it)
+ * for any number of independent evolutions per device.  The Python host
+ * (quantumsimulations_amd/dipolar_ensemble_with_rare.py) reduces a DipolarRareParams to the
+ * coefficient tables taken by dse_add_problem and calls dse_evolve; INTEGRATION.md shows the
+ * ctypes binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - A problem is an n-qubit register, state = 2^n complex doubles, interleaved (re, im).
+ *   - s_b(x) = 1/2 - bit_b(x); bit value 0 = spin up (QuTiP basis(2, 0)).
+ *   - H x-th row:  D(x) psi[x]
+ *                + sum_b flip(b, bit_b(x)) psi[x ^ e_b]
+ *                + sum_{i<j, bit_i(x)==bit_j(x)} pair[i][j] psi[x ^ e_i ^ e_j]
+ *     D(x) = shift + sum_b field[b] s_b(x) + sum_{i<j} zz[i][j] s_i(x) s_j(x).
+ *     flip is given as 4 doubles per bit: (re0, im0, re1, im1) where index v = bit_b(x) is the
+ *     bit value of the OUTPUT row; H must be Hermitian: (re1, im1) = conj(re0, im0).
+ *   - Observables (dse_obs order = the key order of simulate_rare's dict, :671-679):
+ *       Ix_sea, Iy_sea, Iz_sea: sums over the bits of sea_mask;  Iz_R, Ix_R, Iy_R on rare_bit
+ *       (rare_bit < 0: the rare spin is not in the register; Iz_R = rare_z_const, Ix_R = Iy_R = 0);
+ *       state_norm = ||psi||.  Expectations are of the normalised state (QuTiP 5 normalize_output).
+ *   - Status: 0 = ok, negative = error; dse_last_error(ctx) has the message.  No C++ exception
+ *     crosses this boundary.
+ *   - Threading: a context is bound to one device and is not thread-safe; distinct contexts are.
+ *     Calls block until results are in host memory.
+ */
+#ifndef DSE_H
+#define DSE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSE_ABI_VERSION 1
+#define DSE_MAX_QUBITS 34
+#define DSE_N_OBS 7
+
+enum dse_status {
+  DSE_OK = 0,
+  DSE_ERR_ARG = -1,         /* invalid argument (reference: ValueError, :620-621)           */
+  DSE_ERR_OOM = -2,         /* device or host allocation failed                             */
+  DSE_ERR_HIP = -3,         /* HIP runtime error                                             */
+  DSE_ERR_CONVERGENCE = -4, /* Chebyshev degree cap exceeded (reference: sesolve failure)    */
+  DSE_ERR_STATE = -5,       /* call order (e.g. dse_get_state before dse_evolve)             */
+  DSE_ERR_NODEVICE = -6     /* no HIP device / bad device index                             */
+};
+
+enum dse_obs {
+  DSE_OBS_IX_SEA = 0,
+  DSE_OBS_IY_SEA = 1,
+  DSE_OBS_IZ_SEA = 2,
+  DSE_OBS_IZ_R = 3,
+  DSE_OBS_IX_R = 4,
+  DSE_OBS_IY_R = 5,
+  DSE_OBS_NORM = 6
+};
+
+typedef struct dse_ctx dse_ctx;
+
+/* Per-call counters filled by dse_evolve (all sums over every problem of the context). */
+typedef struct dse_stats {
+  double h_applications;      /* Chebyshev terms = applications of H, summed over problems     */
+  double amplitude_updates;   /* sum over step launches of the amplitudes they updated          */
+  double step_bytes;          /* algorithmic HBM bytes of the Chebyshev step kernel (80 B/amp)  */
+  double step_kernel_ms;      /* summed HIP-event time of the step kernel launches              */
+  double step_launches;       /* number of step kernel launches                                 */
+  double obs_kernel_ms;       /* summed HIP-event time of the observable kernel launches        */
+  double wall_ms;             /* host wall time of the call                                     */
+  int32_t max_degree;         /* largest Chebyshev degree of any problem / interval             */
+  int32_t n_intervals;        /* output intervals propagated                                    */
+  int32_t tile_bits;          /* LDS tile used (log2 amplitudes per workgroup)                  */
+  int32_t reserved;
+} dse_stats;
+
+/* ---- library / device ------------------------------------------------------------------- */
+int dse_abi_version(void);
+int dse_device_count(void);                 /* number of HIP devices, 0 if none              */
+
+/* ---- host-only helpers (no device needed; also used by the tests) ------------------------- */
+/* Rigorous spectral bounds of the H defined by the tables (Weyl's inequality over the 1- and
+ * 2-qubit pieces; exact for the non-interacting part).  Arrays as in dse_add_problem. */
+int dse_spectral_bounds(int n_qubits, const double* field, const double* zz, const double* pair,
+                        const double* flip, double shift, double* e_min, double* e_max);
+/* Bessel J_k(z), k = 0..kmax (Miller's backward recurrence, normalised by
+ * J_0 + 2 sum J_2k = 1).  *degree = the Chebyshev truncation degree for tolerance tol
+ * (largest k with |J_k(z)| > tol, at least 1). */
+int dse_bessel_j(double z, int kmax, double* out, double tol, int* degree);
+
+/* ---- context ------------------------------------------------------------------------------ */
+dse_ctx* dse_create(int device);            /* NULL on failure, see dse_create_error()       */
+const char* dse_create_error(void);
+void dse_destroy(dse_ctx* ctx);
+const char* dse_last_error(const dse_ctx* ctx);
+/* Options: "tile_bits" (LDS tile, 6..13, default 12), "time_kernels" (0/1, default 1),
+ *          "max_degree" (Chebyshev degree cap per interval, default 2e6). */
+int dse_set_option(dse_ctx* ctx, const char* key, double value);
+
+/* ---- problems ----------------------------------------------------------------------------- */
+/* Adds an evolution to the context.  field[n], zz[n*n] and pair[n*n] (row-major, upper
+ * triangle i<j read), flip[4n].  Returns the problem id (>= 0) or a negative status. */
+int dse_add_problem(dse_ctx* ctx, int n_qubits, const double* field, const double* zz,
+                    const double* pair, const double* flip, double shift, uint64_t psi0_index,
+                    uint64_t sea_mask, int rare_bit, double rare_z_const);
+int dse_num_problems(const dse_ctx* ctx);
+int dse_clear(dse_ctx* ctx);
+
+/* ---- hot path ----------------------------------------------------------------------------- */
+/* psi_out = H psi_in for one problem (interleaved complex, 2^n each).  Test/diagnostic hook:
+ * runs the same matrix-free tile kernel as the propagator. */
+int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out);
+/* The 7 observables of an arbitrary state of one problem (same kernel as dse_evolve). */
+int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7);
+/* Evolves every problem from its basis state psi0 at t[0] through the output times t[0..n_t)
+ * (strictly increasing) with an exact Chebyshev propagator (truncation tolerance tol, e.g.
+ * 1e-14) and writes obs_out[problem][DSE_N_OBS][n_t].  stats may be NULL. */
+int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out,
+               dse_stats* stats);
+/* Final state of one problem after dse_evolve (2^n interleaved complex). */
+int dse_get_state(dse_ctx* ctx, int problem, double* psi_out);
+/* Times the Chebyshev step kernel alone: reps launches over all problems, HIP events around
+ * each launch.  Returns the mean launch duration and the algorithmic bytes per launch. */
+int dse_time_step_kernel(dse_ctx* ctx, int reps, double* ms_per_launch, double* bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSE_H */

@@ -1,0 +1,105 @@
+"""ctypes binding of libdse.so (include/dse.h).
+
+Loading fails loudly: there is no CPU fallback for the hot path.  Build the
+library with ``python -m quantumsimulations_amd.build`` (``__graft_entry__.build``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdse.so")
+
+DSE_OK = 0
+DSE_ERR_ARG = -1
+DSE_ERR_OOM = -2
+DSE_ERR_HIP = -3
+DSE_ERR_CONVERGENCE = -4
+DSE_ERR_STATE = -5
+DSE_ERR_NODEVICE = -6
+DSE_N_OBS = 7
+DSE_ABI_VERSION = 1
+
+EXPORTED = (
+    "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
+    "dse_create", "dse_create_error", "dse_destroy", "dse_last_error", "dse_set_option",
+    "dse_add_problem", "dse_num_problems", "dse_clear", "dse_apply_h", "dse_observables",
+    "dse_evolve", "dse_get_state", "dse_time_step_kernel",
+)
+
+
+class DseStats(C.Structure):
+    _fields_ = [
+        ("h_applications", C.c_double),
+        ("amplitude_updates", C.c_double),
+        ("step_bytes", C.c_double),
+        ("step_kernel_ms", C.c_double),
+        ("step_launches", C.c_double),
+        ("obs_kernel_ms", C.c_double),
+        ("wall_ms", C.c_double),
+        ("max_degree", C.c_int32),
+        ("n_intervals", C.c_int32),
+        ("tile_bits", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+
+
+_lock = threading.Lock()
+_lib = None
+
+_dp = C.POINTER(C.c_double)
+_vp = C.c_void_p
+
+
+def _declare(lib):
+    sig = {
+        "dse_abi_version": (C.c_int, []),
+        "dse_device_count": (C.c_int, []),
+        "dse_spectral_bounds": (C.c_int, [C.c_int, _dp, _dp, _dp, _dp, C.c_double, _dp, _dp]),
+        "dse_bessel_j": (C.c_int, [C.c_double, C.c_int, _dp, C.c_double, C.POINTER(C.c_int)]),
+        "dse_create": (_vp, [C.c_int]),
+        "dse_create_error": (C.c_char_p, []),
+        "dse_destroy": (None, [_vp]),
+        "dse_last_error": (C.c_char_p, [_vp]),
+        "dse_set_option": (C.c_int, [_vp, C.c_char_p, C.c_double]),
+        "dse_add_problem": (C.c_int, [_vp, C.c_int, _dp, _dp, _dp, _dp, C.c_double, C.c_uint64,
+                                      C.c_uint64, C.c_int, C.c_double]),
+        "dse_num_problems": (C.c_int, [_vp]),
+        "dse_clear": (C.c_int, [_vp]),
+        "dse_apply_h": (C.c_int, [_vp, C.c_int, _dp, _dp]),
+        "dse_observables": (C.c_int, [_vp, C.c_int, _dp, _dp]),
+        "dse_evolve": (C.c_int, [_vp, _dp, C.c_int, C.c_double, _dp, C.POINTER(DseStats)]),
+        "dse_get_state": (C.c_int, [_vp, C.c_int, _dp]),
+        "dse_time_step_kernel": (C.c_int, [_vp, C.c_int, _dp, _dp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """The loaded library (raises ImportError if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} is missing: build it with `python -m quantumsimulations_amd.build` "
+                    "(the HIP engine has no CPU fallback)")
+            handle = C.CDLL(LIB_PATH)
+            _declare(handle)
+            if handle.dse_abi_version() != DSE_ABI_VERSION:
+                raise ImportError("libdse.so ABI version mismatch; rebuild it")
+            _lib = handle
+    return _lib
+
+
+def ptr(a):
+    """double* of a contiguous float64/complex128 numpy array."""
+    return a.ctypes.data_as(_dp)

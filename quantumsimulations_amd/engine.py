@@ -1,0 +1,147 @@
+"""Python handle on one device's engine context (libdse.so).
+
+``Engine`` owns a ``dse_ctx``: problems (coefficient tables from ``problem.py``)
+are added, then evolved together on one MI355X with the exact Chebyshev
+propagator.  Errors from the library surface as ``ValueError`` (bad arguments,
+as the reference raises for a bad grid, dipolar_ensemble_with_rare.py:620-621)
+or ``RuntimeError`` (HIP / allocation / degree-cap failures).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Tuple
+
+import numpy as np
+
+from . import _lib
+from .problem import Problem
+
+DEFAULT_TOL = 1e-14
+
+
+def device_count() -> int:
+    return int(_lib.lib().dse_device_count())
+
+
+class Engine:
+    def __init__(self, device: int = 0, tile_bits: int | None = None, time_kernels: bool = True):
+        self._L = _lib.lib()
+        h = self._L.dse_create(int(device))
+        if not h:
+            raise RuntimeError("dse_create failed: " + self._L.dse_create_error().decode())
+        self._h = C.c_void_p(h)
+        self.device = device
+        self.problems: list[Problem] = []
+        if tile_bits is not None:
+            self.set_option("tile_bits", tile_bits)
+        self.set_option("time_kernels", 1.0 if time_kernels else 0.0)
+
+    # -- plumbing --
+    def _check(self, rc: int) -> int:
+        if rc >= 0:
+            return rc
+        msg = self._L.dse_last_error(self._h).decode()
+        if rc == _lib.DSE_ERR_ARG:
+            raise ValueError(msg)
+        raise RuntimeError(f"libdse error {rc}: {msg}")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.dse_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_option(self, key: str, value: float) -> None:
+        self._check(self._L.dse_set_option(self._h, key.encode(), float(value)))
+
+    # -- problems --
+    def add(self, prob: Problem) -> int:
+        n = prob.n_qubits
+        field = np.ascontiguousarray(prob.field, dtype=np.float64)
+        zz = np.ascontiguousarray(prob.zz, dtype=np.float64).reshape(n * n)
+        pair = np.ascontiguousarray(prob.pair, dtype=np.float64).reshape(n * n)
+        flip = np.ascontiguousarray(prob.flip, dtype=np.float64).reshape(4 * n)
+        pid = self._check(self._L.dse_add_problem(
+            self._h, n, _lib.ptr(field), _lib.ptr(zz), _lib.ptr(pair), _lib.ptr(flip),
+            float(prob.shift), int(prob.psi0_index), int(prob.sea_mask), int(prob.rare_bit),
+            float(prob.rare_z_const)))
+        self.problems.append(prob)
+        return pid
+
+    def clear(self) -> None:
+        self._check(self._L.dse_clear(self._h))
+        self.problems = []
+
+    # -- hot path --
+    def apply_h(self, pid: int, psi: np.ndarray) -> np.ndarray:
+        n = self.problems[pid].n_qubits
+        x = np.ascontiguousarray(psi, dtype=np.complex128)
+        if x.shape != (1 << n,):
+            raise ValueError(f"state must have shape ({1 << n},)")
+        out = np.empty_like(x)
+        self._check(self._L.dse_apply_h(self._h, pid, _lib.ptr(x), _lib.ptr(out)))
+        return out
+
+    def observables(self, pid: int, psi: np.ndarray) -> np.ndarray:
+        n = self.problems[pid].n_qubits
+        x = np.ascontiguousarray(psi, dtype=np.complex128)
+        if x.shape != (1 << n,):
+            raise ValueError(f"state must have shape ({1 << n},)")
+        out = np.empty(7)
+        self._check(self._L.dse_observables(self._h, pid, _lib.ptr(x), _lib.ptr(out)))
+        return out
+
+    def evolve(self, t: np.ndarray, tol: float = DEFAULT_TOL) -> Tuple[np.ndarray, Dict[str, float]]:
+        """obs[problem, 7, n_t] for all problems, and the call's counters."""
+        tt = np.ascontiguousarray(t, dtype=np.float64)
+        out = np.empty((len(self.problems), _lib.DSE_N_OBS, len(tt)))
+        st = _lib.DseStats()
+        self._check(self._L.dse_evolve(self._h, _lib.ptr(tt), len(tt), float(tol), _lib.ptr(out),
+                                       C.byref(st)))
+        return out, st.as_dict()
+
+    def state(self, pid: int) -> np.ndarray:
+        n = self.problems[pid].n_qubits
+        out = np.empty(1 << n, dtype=np.complex128)
+        self._check(self._L.dse_get_state(self._h, pid, _lib.ptr(out)))
+        return out
+
+    def time_step_kernel(self, reps: int = 20) -> Tuple[float, float]:
+        ms = C.c_double()
+        by = C.c_double()
+        self._check(self._L.dse_time_step_kernel(self._h, int(reps), C.byref(ms), C.byref(by)))
+        return ms.value, by.value
+
+
+def spectral_bounds_native(prob: Problem) -> Tuple[float, float]:
+    """dse_spectral_bounds (host-only library function)."""
+    L = _lib.lib()
+    n = prob.n_qubits
+    arrs = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in (prob.field, prob.zz, prob.pair, prob.flip)]
+    lo, hi = C.c_double(), C.c_double()
+    rc = L.dse_spectral_bounds(n, *[_lib.ptr(a) for a in arrs], float(prob.shift), C.byref(lo), C.byref(hi))
+    if rc != 0:
+        raise ValueError("dse_spectral_bounds failed")
+    return lo.value, hi.value
+
+
+def bessel_native(z: float, kmax: int, tol: float = 1e-14) -> Tuple[np.ndarray, int]:
+    """dse_bessel_j (host-only library function): J_0..J_kmax(z) and the truncation degree."""
+    L = _lib.lib()
+    out = np.empty(kmax + 1)
+    deg = C.c_int()
+    rc = L.dse_bessel_j(float(z), int(kmax), _lib.ptr(out), float(tol), C.byref(deg))
+    if rc != 0:
+        raise ValueError("dse_bessel_j failed")
+    return out, deg.value
