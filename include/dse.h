@@ -68,15 +68,16 @@ typedef struct dse_ctx dse_ctx;
 typedef struct dse_stats {
   double h_applications;      /* Chebyshev terms = applications of H, summed over problems     */
   double amplitude_updates;   /* sum over step launches of the amplitudes they updated          */
-  double step_bytes;          /* algorithmic HBM bytes of the Chebyshev step kernel (80 B/amp)  */
-  double step_kernel_ms;      /* summed HIP-event time of the step kernel launches              */
-  double step_launches;       /* number of step kernel launches                                 */
-  double obs_kernel_ms;       /* summed HIP-event time of the observable kernel launches        */
+  double step_bytes;          /* algorithmic HBM bytes of all step launches (80 B / amplitude)  */
+  double step_kernel_ms;      /* summed HIP-event time of the timed step launches (-1: none)    */
+  double step_launches;       /* number of step kernel launches (k >= 2)                        */
+  double timed_launches;      /* step launches bracketed by HIP events                          */
+  double timed_bytes;         /* algorithmic bytes of the timed launches                        */
   double wall_ms;             /* host wall time of the call                                     */
   int32_t max_degree;         /* largest Chebyshev degree of any problem / interval             */
   int32_t n_intervals;        /* output intervals propagated                                    */
-  int32_t tile_bits;          /* LDS tile used (log2 amplitudes per workgroup)                  */
-  int32_t reserved;
+  int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
+  int32_t streams;            /* HIP streams ("lanes") the problems were spread over            */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -98,8 +99,11 @@ dse_ctx* dse_create(int device);            /* NULL on failure, see dse_create_e
 const char* dse_create_error(void);
 void dse_destroy(dse_ctx* ctx);
 const char* dse_last_error(const dse_ctx* ctx);
-/* Options: "tile_bits" (LDS tile, 6..13, default 12), "time_kernels" (0/1, default 1),
- *          "max_degree" (Chebyshev degree cap per interval, default 2e6). */
+/* Options: "tile_bits"    LDS tile, log2 amplitudes per workgroup, 1..13 (default 13)
+ *          "streams"      HIP streams the problems are spread over, 1..16 (default 4)
+ *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
+ *                         HIP events (default 1)
+ *          "max_degree"   Chebyshev degree cap per interval (default 2e6) */
 int dse_set_option(dse_ctx* ctx, const char* key, double value);
 
 /* ---- problems ----------------------------------------------------------------------------- */

@@ -37,16 +37,17 @@ class DseStats(C.Structure):
         ("step_bytes", C.c_double),
         ("step_kernel_ms", C.c_double),
         ("step_launches", C.c_double),
-        ("obs_kernel_ms", C.c_double),
+        ("timed_launches", C.c_double),
+        ("timed_bytes", C.c_double),
         ("wall_ms", C.c_double),
         ("max_degree", C.c_int32),
         ("n_intervals", C.c_int32),
         ("tile_bits", C.c_int32),
-        ("reserved", C.c_int32),
+        ("streams", C.c_int32),
     ]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 _lock = threading.Lock()

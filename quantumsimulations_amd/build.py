@@ -16,7 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdse.so")
-SOURCES = ["dse.hip", "dse_host.cpp"]
+SOURCES = ["dse_kernels.hip", "dse_runtime.hip", "dse_host.cpp"]
+HEADERS = ["dse_internal.h"]
 ARCH = os.environ.get("DSE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -31,7 +32,7 @@ def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(ROOT, "include", "dse.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "dse.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

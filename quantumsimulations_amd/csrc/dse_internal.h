@@ -1,0 +1,85 @@
+// dse_internal.h -- device-side data structures shared by the kernels and the runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dse {
+
+enum { MODE_APPLY = 0, MODE_FIRST = 1, MODE_GEN = 2 };
+
+constexpr int kMinTile = 1;
+constexpr int kMaxTile = 13;
+constexpr int kRegBlockMinTile = 9;  // tiles >= 2^9 use the register-block kernel
+constexpr int kRegBits = 3;          // amplitudes per thread = 2^kRegBits in that kernel
+
+// A pair flip or a drive flip, split into its in-tile mask and its tile-index mask.
+//   pair : applies iff bit_i(x) == bit_j(x) <=> popc(x_lo & mask_lo) + popc(h & tile_xor) even
+//   flip : coefficient index v = parity(x_lo & mask_lo) ^ parity(h & tile_xor) (output bit value)
+struct alignas(16) DPair {
+  uint32_t mask_lo;
+  uint32_t tile_xor;
+  double g;
+};
+struct alignas(16) DFlip {
+  uint32_t mask_lo;
+  uint32_t tile_xor;
+  double re0, im0, re1, im1;
+  double pad;
+};
+
+// Register-block kernel: one thread owns the 8 amplitudes x = rho * NT + tid (rho = 0..7),
+// i.e. the three top tile bits are "register bits".  For every thread bit j a sweep reads the
+// partner thread's 8 amplitudes once from LDS and applies (a) the drive flip of bit j and
+// (b) the pair flips (j, register bit i) for i = 0..2.
+struct alignas(16) DSweep {
+  double re0, im0, re1, im1;  // drive flip on thread bit j (zero when absent)
+  double g[3];                // pair coefficient with register bit i
+  uint32_t has_flip;
+  uint32_t has_pair;
+};
+
+// Chebyshev coefficients of one term k for one interval length.  The propagator sum
+// acc = sum_k a_k w_k is accumulated every third term (and at the last term) from the three
+// vectors the step kernel holds anyway: acc += c[0] w_{k-2} + c[1] w_{k-1} + c[2] w_k.
+// MODE_FIRST (k = 1) writes acc = c[1] w_0 + c[2] w_1.
+struct alignas(16) CoefK {
+  double2 c[3];
+  int upd;
+  int pad[3];
+};
+
+struct DevProb {
+  double2* buf[3];
+  const double* zzlo;     // [2^L]  sum_{i<j<L} zz_ij s_i s_j
+  const double* field;    // [n]
+  const double* zz;       // [n*n]
+  const DPair* pairs_lo;  // generic kernel: both bits inside the tile
+  const DPair* pairs_hi;  // at least one bit above the tile (both kernels)
+  const DFlip* flips_lo;  // generic kernel
+  const DFlip* flips_hi;  // both kernels
+  const DSweep* sweeps;   // register-block kernel: [L-3] thread-bit sweeps
+  const DPair* pairs_tt;  // register-block kernel: pairs between two thread bits
+  const CoefK* coef;      // [n_sets][kcap1] Chebyshev coefficients per term
+  uint64_t sea_mask;
+  double shift;
+  double beta;            // spectral centre
+  double s1;              // 1/alpha
+  double rr_g[3];         // register-block kernel: pairs (0,1) (0,2) (1,2) among register bits
+  double rflip[3][4];     // register-block kernel: drive flips on register bits (re0 im0 re1 im1)
+  int n, L;
+  int n_pairs_lo, n_pairs_hi, n_flips_lo, n_flips_hi, n_pairs_tt;
+  int kcap1;
+  int degree;             // Chebyshev degree K of the current evolve (terms k = 1..K)
+  int rare_bit;
+  int n_sea;
+  int rflip_mask;         // bit i set: register bit i has a drive flip
+};
+
+hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items, int n_items,
+                       int k, int q, int set, hipStream_t st);
+hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
+                      double* partial, hipStream_t st);
+
+}  // namespace dse

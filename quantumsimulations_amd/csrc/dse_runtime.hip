@@ -1,0 +1,886 @@
+// dse_runtime.hip -- host runtime behind the C ABI of include/dse.h.
+//
+// Replaces qt.sesolve (dipolar_ensemble_with_rare.py:653-666) for many independent evolutions
+// per device.  Per output interval [t_m, t_{m+1}] every problem runs
+//     k = 1 (MODE_FIRST), k = 2..K_p (MODE_GEN), observables of the new state
+// on one of several HIP streams ("lanes").  Problems are independent, so lanes never
+// synchronise with each other until observable partials are copied back; the GPU overlaps
+// the tail of one lane's launch with the next launches of the others.  Within a lane,
+// items (problem, tile) are sorted by Chebyshev degree so the items still active at term k are
+// a prefix of the lane's item list.
+//
+// HBM layout per problem: three 2^n double2 state buffers B0, B1, B2.  In interval m (parity q):
+//   psi = B[q ? 2 : 0], acc = B[q ? 0 : 2], scratch = B1;  w_j lives in (j odd ? scratch : psi)
+// and MODE_GEN overwrites w_{k-2} in place with w_k.  At the end of the interval acc holds
+// psi(t_{m+1}) and becomes psi of the next interval.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <complex>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/dse.h"
+#include "dse_internal.h"
+
+using namespace dse;
+
+namespace {
+
+struct HostProblem {
+  int n = 0;
+  std::vector<double> field, zz, pair, flip;
+  double shift = 0.0;
+  uint64_t psi0 = 0, sea_mask = 0;
+  int rare_bit = -1;
+  double rare_z = 0.0;
+  double e_min = 0.0, e_max = 0.0;
+  // device state
+  int L = 0;
+  int64_t n_tiles = 0;
+  double2* buf[3] = {nullptr, nullptr, nullptr};
+  void* tables = nullptr;
+  CoefK* coef = nullptr;
+  size_t coef_bytes = 0;
+  int degree = 1;
+  int2* d_items = nullptr;  // this problem's tiles (apply_h / observables hooks)
+};
+
+// One stream's share of the problems, grouped by tile size.
+struct LaneGroup {
+  int L = 0;
+  int64_t off = 0;          // first position in the global item array
+  int64_t count = 0;        // items of this group
+  std::vector<int> active;     // active[k] = items with degree >= k (prefix of the group)
+  std::vector<double> bytes;   // bytes[k] = algorithmic HBM bytes of the term-k launch
+};
+struct Lane {
+  hipStream_t stream = nullptr;
+  std::vector<LaneGroup> groups;
+  std::vector<hipEvent_t> ev[2];
+  size_t ev_used[2] = {0, 0};
+  int max_deg = 0;
+};
+
+}  // namespace
+
+struct dse_ctx {
+  int device = 0;
+  std::string err;
+  std::vector<HostProblem> probs;
+  DevProb* d_probs = nullptr;
+  std::vector<DevProb> h_desc;
+  std::vector<Lane> lanes;
+  int2* d_items = nullptr;          // all items, lane-major, degree-sorted inside each group
+  std::vector<int64_t> item_pos;    // first item position of every problem (evolve layout)
+  int64_t total_items = 0;
+  double* d_partial = nullptr;
+  size_t partial_slots = 0;
+  std::map<std::vector<double>, double*> zzlo_tables;  // identical in-tile ZZ tables are shared
+  bool prepared = false;
+  bool evolved = false;
+  int last_q = 0;
+  int tile_bits = 13;
+  int n_streams = 4;
+  int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
+  double max_degree = 2e6;
+};
+
+namespace {
+
+thread_local std::string g_create_err;
+
+int fail(dse_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPC(expr)                                                                      \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return fail(ctx, DSE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+void free_device(dse_ctx* ctx) {
+  for (auto& p : ctx->probs) {
+    for (auto& b : p.buf)
+      if (b) (void)hipFree(b), b = nullptr;
+    if (p.tables) (void)hipFree(p.tables), p.tables = nullptr;
+    if (p.coef) (void)hipFree(p.coef), p.coef = nullptr;
+    if (p.d_items) (void)hipFree(p.d_items), p.d_items = nullptr;
+    p.coef_bytes = 0;
+  }
+  if (ctx->d_probs) (void)hipFree(ctx->d_probs), ctx->d_probs = nullptr;
+  if (ctx->d_items) (void)hipFree(ctx->d_items), ctx->d_items = nullptr;
+  if (ctx->d_partial) (void)hipFree(ctx->d_partial), ctx->d_partial = nullptr;
+  for (auto& kv : ctx->zzlo_tables) (void)hipFree(kv.second);
+  ctx->zzlo_tables.clear();
+  ctx->partial_slots = 0;
+  ctx->total_items = 0;
+  ctx->prepared = false;
+  ctx->evolved = false;
+}
+
+void destroy_lanes(dse_ctx* ctx) {
+  for (auto& ln : ctx->lanes) {
+    if (ln.stream) (void)hipStreamSynchronize(ln.stream);
+    for (auto& pool : ln.ev)
+      for (auto e : pool) (void)hipEventDestroy(e);
+    if (ln.stream) (void)hipStreamDestroy(ln.stream);
+  }
+  ctx->lanes.clear();
+}
+
+int ensure_lanes(dse_ctx* ctx) {
+  if ((int)ctx->lanes.size() == ctx->n_streams) return DSE_OK;
+  destroy_lanes(ctx);
+  ctx->lanes.resize(ctx->n_streams);
+  for (auto& ln : ctx->lanes) HIPC(hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
+  return DSE_OK;
+}
+
+int sync_all(dse_ctx* ctx) {
+  for (auto& ln : ctx->lanes) HIPC(hipStreamSynchronize(ln.stream));
+  return DSE_OK;
+}
+
+// ---- per-problem device tables ------------------------------------------------------------
+int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
+  const int n = p.n;
+  const int L = std::max(std::min(n, ctx->tile_bits), std::max(kMinTile, n - 32));
+  if (L > kMaxTile) return fail(ctx, DSE_ERR_ARG, "problem too large for the tile range");
+  p.L = L;
+  p.n_tiles = int64_t(1) << (n - L);
+  const size_t T = size_t(1) << L;
+  const uint64_t lo_mask = (uint64_t(1) << L) - 1;
+  const bool rb = L >= kRegBlockMinTile;
+  const int TB = L - kRegBits;
+
+  std::vector<double> zzlo(T, 0.0);
+  for (size_t x = 0; x < T; ++x) {
+    double acc = 0.0;
+    for (int i = 0; i < L; ++i) {
+      const double si = 0.5 - (double)((x >> i) & 1);
+      for (int j = i + 1; j < L; ++j) acc += p.zz[i * n + j] * (si * (0.5 - (double)((x >> j) & 1)));
+    }
+    zzlo[x] = acc;
+  }
+  std::memset(&d, 0, sizeof(d));
+  std::vector<DPair> plo, phi, ptt;
+  std::vector<DFlip> flo, fhi;
+  std::vector<DSweep> sweeps(rb ? TB : 0);
+  for (auto& s : sweeps) std::memset(&s, 0, sizeof(s));
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const double g = p.pair[i * n + j];
+      if (g == 0.0) continue;
+      const uint64_t m = (uint64_t(1) << i) | (uint64_t(1) << j);
+      DPair q;
+      q.mask_lo = (uint32_t)(m & lo_mask);
+      q.tile_xor = (uint32_t)(m >> L);
+      q.g = g;
+      if (q.tile_xor) {
+        phi.push_back(q);
+      } else if (!rb) {
+        plo.push_back(q);
+      } else if (j < TB) {
+        ptt.push_back(q);  // both thread bits
+      } else if (i >= TB) {
+        const int a = i - TB, b = j - TB;  // both register bits: (0,1) (0,2) (1,2)
+        d.rr_g[(a == 0 && b == 1) ? 0 : (a == 0 ? 1 : 2)] = g;
+      } else {
+        sweeps[i].g[j - TB] = g;  // thread bit i, register bit j - TB
+        sweeps[i].has_pair = 1;
+      }
+    }
+  for (int b = 0; b < n; ++b) {
+    const double* f = &p.flip[4 * b];
+    if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
+    const uint64_t m = uint64_t(1) << b;
+    DFlip q;
+    q.mask_lo = (uint32_t)(m & lo_mask);
+    q.tile_xor = (uint32_t)(m >> L);
+    q.re0 = f[0];
+    q.im0 = f[1];
+    q.re1 = f[2];
+    q.im1 = f[3];
+    q.pad = 0.0;
+    if (q.tile_xor) {
+      fhi.push_back(q);
+    } else if (!rb) {
+      flo.push_back(q);
+    } else if (b < TB) {
+      DSweep& s = sweeps[b];
+      s.re0 = f[0];
+      s.im0 = f[1];
+      s.re1 = f[2];
+      s.im1 = f[3];
+      s.has_flip = 1;
+    } else {
+      const int i = b - TB;
+      for (int c = 0; c < 4; ++c) d.rflip[i][c] = f[c];
+      d.rflip_mask |= 1 << i;
+    }
+  }
+  const size_t o_field = 0;
+  const size_t o_zz = align_up(o_field + n * sizeof(double), 256);
+  const size_t o_plo = align_up(o_zz + size_t(n) * n * sizeof(double), 256);
+  const size_t o_phi = align_up(o_plo + plo.size() * sizeof(DPair), 256);
+  const size_t o_ptt = align_up(o_phi + phi.size() * sizeof(DPair), 256);
+  const size_t o_flo = align_up(o_ptt + ptt.size() * sizeof(DPair), 256);
+  const size_t o_fhi = align_up(o_flo + flo.size() * sizeof(DFlip), 256);
+  const size_t o_sw = align_up(o_fhi + fhi.size() * sizeof(DFlip), 256);
+  const size_t total = align_up(o_sw + sweeps.size() * sizeof(DSweep) + 16, 256);
+  std::vector<char> blob(total, 0);
+  auto put = [&](size_t off, const void* src, size_t bytes) {
+    if (bytes) std::memcpy(blob.data() + off, src, bytes);
+  };
+  put(o_field, p.field.data(), n * sizeof(double));
+  put(o_zz, p.zz.data(), size_t(n) * n * sizeof(double));
+  put(o_plo, plo.data(), plo.size() * sizeof(DPair));
+  put(o_phi, phi.data(), phi.size() * sizeof(DPair));
+  put(o_ptt, ptt.data(), ptt.size() * sizeof(DPair));
+  put(o_flo, flo.data(), flo.size() * sizeof(DFlip));
+  put(o_fhi, fhi.data(), fhi.size() * sizeof(DFlip));
+  put(o_sw, sweeps.data(), sweeps.size() * sizeof(DSweep));
+  if (hipMalloc(&p.tables, total) != hipSuccess)
+    return fail(ctx, DSE_ERR_OOM, "device allocation of coefficient tables failed");
+  HIPC(hipMemcpy(p.tables, blob.data(), total, hipMemcpyHostToDevice));
+  const size_t vbytes = (size_t(1) << n) * sizeof(double2);
+  for (auto& b : p.buf) {
+    if (hipMalloc(&b, vbytes) != hipSuccess)
+      return fail(ctx, DSE_ERR_OOM, "device allocation of state buffers failed (" +
+                                        std::to_string(3 * vbytes) + " bytes per problem)");
+    HIPC(hipMemset(b, 0, vbytes));
+  }
+  char* tb = static_cast<char*>(p.tables);
+  for (int i = 0; i < 3; ++i) d.buf[i] = p.buf[i];
+  auto zt = ctx->zzlo_tables.find(zzlo);
+  if (zt == ctx->zzlo_tables.end()) {
+    double* dz = nullptr;
+    if (hipMalloc(&dz, T * sizeof(double)) != hipSuccess)
+      return fail(ctx, DSE_ERR_OOM, "device allocation of the ZZ table failed");
+    HIPC(hipMemcpy(dz, zzlo.data(), T * sizeof(double), hipMemcpyHostToDevice));
+    zt = ctx->zzlo_tables.emplace(zzlo, dz).first;
+  }
+  d.zzlo = zt->second;
+  d.field = reinterpret_cast<const double*>(tb + o_field);
+  d.zz = reinterpret_cast<const double*>(tb + o_zz);
+  d.pairs_lo = reinterpret_cast<const DPair*>(tb + o_plo);
+  d.pairs_hi = reinterpret_cast<const DPair*>(tb + o_phi);
+  d.pairs_tt = reinterpret_cast<const DPair*>(tb + o_ptt);
+  d.flips_lo = reinterpret_cast<const DFlip*>(tb + o_flo);
+  d.flips_hi = reinterpret_cast<const DFlip*>(tb + o_fhi);
+  d.sweeps = reinterpret_cast<const DSweep*>(tb + o_sw);
+  d.coef = nullptr;
+  d.sea_mask = p.sea_mask;
+  d.shift = p.shift;
+  d.beta = 0.0;
+  d.s1 = 1.0;
+  d.n = n;
+  d.L = L;
+  d.n_pairs_lo = (int)plo.size();
+  d.n_pairs_hi = (int)phi.size();
+  d.n_pairs_tt = (int)ptt.size();
+  d.n_flips_lo = (int)flo.size();
+  d.n_flips_hi = (int)fhi.size();
+  d.kcap1 = 0;
+  d.rare_bit = p.rare_bit;
+  d.n_sea = __builtin_popcountll(p.sea_mask);
+  return DSE_OK;
+}
+
+int prepare(dse_ctx* ctx) {
+  if (ctx->prepared) return DSE_OK;
+  if (ctx->probs.empty()) return fail(ctx, DSE_ERR_STATE, "no problems added");
+  int rc = ensure_lanes(ctx);
+  if (rc) return rc;
+  std::vector<DevProb> dp(ctx->probs.size());
+  int64_t total = 0;
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    if ((rc = build_tables(ctx, ctx->probs[pi], dp[pi]))) {
+      free_device(ctx);
+      return rc;
+    }
+    HostProblem& p = ctx->probs[pi];
+    std::vector<int2> its(p.n_tiles);
+    for (int64_t t = 0; t < p.n_tiles; ++t) its[t] = make_int2((int)pi, (int)t);
+    if (hipMalloc(&p.d_items, its.size() * sizeof(int2)) != hipSuccess) {
+      free_device(ctx);
+      return fail(ctx, DSE_ERR_OOM, "device allocation of item lists failed");
+    }
+    HIPC(hipMemcpy(p.d_items, its.data(), its.size() * sizeof(int2), hipMemcpyHostToDevice));
+    total += p.n_tiles;
+  }
+  if (hipMalloc(&ctx->d_probs, dp.size() * sizeof(DevProb)) != hipSuccess ||
+      hipMalloc(&ctx->d_items, total * sizeof(int2)) != hipSuccess) {
+    free_device(ctx);
+    return fail(ctx, DSE_ERR_OOM, "device allocation of descriptors failed");
+  }
+  HIPC(hipMemcpy(ctx->d_probs, dp.data(), dp.size() * sizeof(DevProb), hipMemcpyHostToDevice));
+  ctx->h_desc = dp;
+  ctx->total_items = total;
+  HIPC(hipDeviceSynchronize());
+  ctx->prepared = true;
+  return DSE_OK;
+}
+
+int ensure_partial(dse_ctx* ctx, size_t slots) {
+  if (ctx->partial_slots >= slots) return DSE_OK;
+  if (ctx->d_partial) (void)hipFree(ctx->d_partial), ctx->d_partial = nullptr;
+  if (hipMalloc(&ctx->d_partial, slots * ctx->total_items * 8 * sizeof(double)) != hipSuccess)
+    return fail(ctx, DSE_ERR_OOM, "device allocation of observable partials failed");
+  ctx->partial_slots = slots;
+  return DSE_OK;
+}
+
+void finish_obs(const HostProblem& P, const double* v, double* o, size_t stride) {
+  const double n2 = v[6];
+  const double inv = n2 > 0.0 ? 1.0 / n2 : 0.0;
+  o[0 * stride] = v[0] * inv;
+  o[1 * stride] = v[1] * inv;
+  o[2 * stride] = v[2] * inv;
+  o[3 * stride] = P.rare_bit >= 0 ? v[3] * inv : P.rare_z;
+  o[4 * stride] = P.rare_bit >= 0 ? v[4] * inv : 0.0;
+  o[5 * stride] = P.rare_bit >= 0 ? v[5] * inv : 0.0;
+  o[6 * stride] = std::sqrt(n2);
+}
+
+int flush_partials(dse_ctx* ctx, size_t nslots, size_t t0, int n_t, double* obs_out) {
+  if ((int)sync_all(ctx)) return DSE_ERR_HIP;
+  std::vector<double> h(nslots * ctx->total_items * 8);
+  HIPC(hipMemcpy(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    const HostProblem& P = ctx->probs[pi];
+    const int64_t first = ctx->item_pos[pi];
+    for (size_t s = 0; s < nslots; ++s) {
+      double v[7] = {0, 0, 0, 0, 0, 0, 0};
+      const double* row = h.data() + (s * ctx->total_items + first) * 8;
+      for (int64_t t = 0; t < P.n_tiles; ++t)
+        for (int j = 0; j < 7; ++j) v[j] += row[t * 8 + j];
+      finish_obs(P, v, obs_out + pi * DSE_N_OBS * (size_t)n_t + (t0 + s), (size_t)n_t);
+    }
+  }
+  return DSE_OK;
+}
+
+int ensure_events(dse_ctx* ctx, Lane& ln, size_t per_pool) {
+  for (int p = 0; p < 2; ++p)
+    while (ln.ev[p].size() < 2 * per_pool) {
+      hipEvent_t e;
+      HIPC(hipEventCreate(&e));
+      ln.ev[p].push_back(e);
+    }
+  return DSE_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+int dse_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* dse_create_error(void) { return g_create_err.c_str(); }
+
+dse_ctx* dse_create(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    g_create_err = "no HIP device available";
+    return nullptr;
+  }
+  if (device < 0 || device >= n) {
+    g_create_err = "device index out of range";
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    g_create_err = "hipSetDevice failed";
+    return nullptr;
+  }
+  dse_ctx* ctx = new (std::nothrow) dse_ctx();
+  if (!ctx) {
+    g_create_err = "out of host memory";
+    return nullptr;
+  }
+  ctx->device = device;
+  if (ensure_lanes(ctx) != DSE_OK) {
+    g_create_err = "stream creation failed: " + ctx->err;
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+void dse_destroy(dse_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)sync_all(ctx);
+  free_device(ctx);
+  destroy_lanes(ctx);
+  delete ctx;
+}
+
+const char* dse_last_error(const dse_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dse_set_option(dse_ctx* ctx, const char* key, double value) {
+  if (!ctx || !key) return DSE_ERR_ARG;
+  const std::string k(key);
+  (void)hipSetDevice(ctx->device);
+  if (k == "tile_bits") {
+    if (!(value >= 1 && value <= kMaxTile)) return fail(ctx, DSE_ERR_ARG, "tile_bits must be in 1..13");
+    if ((int)value != ctx->tile_bits) {
+      (void)sync_all(ctx);
+      free_device(ctx);
+      ctx->tile_bits = (int)value;
+    }
+  } else if (k == "streams") {
+    if (!(value >= 1 && value <= 16)) return fail(ctx, DSE_ERR_ARG, "streams must be in 1..16");
+    (void)sync_all(ctx);
+    ctx->n_streams = (int)value;
+    ctx->evolved = false;
+    return ensure_lanes(ctx);
+  } else if (k == "time_kernels") {
+    if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
+    ctx->time_every = (int)value;
+  } else if (k == "max_degree") {
+    if (!(value >= 1)) return fail(ctx, DSE_ERR_ARG, "max_degree must be >= 1");
+    ctx->max_degree = value;
+  } else {
+    return fail(ctx, DSE_ERR_ARG, "unknown option " + k);
+  }
+  return DSE_OK;
+}
+
+int dse_add_problem(dse_ctx* ctx, int n, const double* field, const double* zz, const double* pair,
+                    const double* flip, double shift, uint64_t psi0_index, uint64_t sea_mask,
+                    int rare_bit, double rare_z_const) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (n < 1 || n > DSE_MAX_QUBITS) return fail(ctx, DSE_ERR_ARG, "n_qubits out of range 1..34");
+  if (!field || !zz || !pair || !flip) return fail(ctx, DSE_ERR_ARG, "null coefficient table");
+  const uint64_t dim = uint64_t(1) << n;
+  if (psi0_index >= dim) return fail(ctx, DSE_ERR_ARG, "psi0_index >= 2^n");
+  if ((sea_mask >> n) != 0) return fail(ctx, DSE_ERR_ARG, "sea_mask has bits >= n");
+  if (rare_bit >= n || rare_bit < -1) return fail(ctx, DSE_ERR_ARG, "rare_bit out of range");
+  HostProblem p;
+  p.n = n;
+  p.field.assign(field, field + n);
+  p.zz.assign(zz, zz + size_t(n) * n);
+  p.pair.assign(pair, pair + size_t(n) * n);
+  p.flip.assign(flip, flip + 4 * size_t(n));
+  for (double v : p.field)
+    if (!std::isfinite(v)) return fail(ctx, DSE_ERR_ARG, "non-finite field");
+  for (double v : p.zz)
+    if (!std::isfinite(v)) return fail(ctx, DSE_ERR_ARG, "non-finite zz");
+  for (double v : p.pair)
+    if (!std::isfinite(v)) return fail(ctx, DSE_ERR_ARG, "non-finite pair");
+  for (int b = 0; b < n; ++b) {
+    const double* f = &p.flip[4 * b];
+    if (!(std::isfinite(f[0]) && std::isfinite(f[1]) && std::isfinite(f[2]) && std::isfinite(f[3])))
+      return fail(ctx, DSE_ERR_ARG, "non-finite flip");
+    const double scale = std::fabs(f[0]) + std::fabs(f[1]) + std::fabs(f[2]) + std::fabs(f[3]);
+    if (std::fabs(f[0] - f[2]) > 1e-12 * scale || std::fabs(f[1] + f[3]) > 1e-12 * scale)
+      return fail(ctx, DSE_ERR_ARG, "flip coefficients are not Hermitian (need c1 = conj(c0))");
+  }
+  if (!std::isfinite(shift)) return fail(ctx, DSE_ERR_ARG, "non-finite shift");
+  p.shift = shift;
+  p.psi0 = psi0_index;
+  p.sea_mask = sea_mask;
+  p.rare_bit = rare_bit;
+  p.rare_z = rare_z_const;
+  dse_spectral_bounds(n, p.field.data(), p.zz.data(), p.pair.data(), p.flip.data(), shift, &p.e_min, &p.e_max);
+  (void)hipSetDevice(ctx->device);
+  (void)sync_all(ctx);
+  free_device(ctx);  // device layout is rebuilt lazily
+  ctx->probs.push_back(std::move(p));
+  return (int)ctx->probs.size() - 1;
+}
+
+int dse_num_problems(const dse_ctx* ctx) { return ctx ? (int)ctx->probs.size() : DSE_ERR_ARG; }
+
+int dse_clear(dse_ctx* ctx) {
+  if (!ctx) return DSE_ERR_ARG;
+  (void)hipSetDevice(ctx->device);
+  (void)sync_all(ctx);
+  free_device(ctx);
+  ctx->probs.clear();
+  return DSE_OK;
+}
+
+int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (problem < 0 || problem >= (int)ctx->probs.size()) return fail(ctx, DSE_ERR_ARG, "bad problem id");
+  if (!psi_in || !psi_out) return fail(ctx, DSE_ERR_ARG, "null state");
+  HIPC(hipSetDevice(ctx->device));
+  int rc = prepare(ctx);
+  if (rc) return rc;
+  HostProblem& P = ctx->probs[problem];
+  hipStream_t st = ctx->lanes[0].stream;
+  const size_t bytes = (size_t(1) << P.n) * sizeof(double2);
+  HIPC(hipMemcpyAsync(P.buf[0], psi_in, bytes, hipMemcpyHostToDevice, st));
+  HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+  HIPC(hipMemcpyAsync(psi_out, P.buf[1], bytes, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  ctx->evolved = false;
+  return DSE_OK;
+}
+
+int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (problem < 0 || problem >= (int)ctx->probs.size()) return fail(ctx, DSE_ERR_ARG, "bad problem id");
+  if (!psi || !obs7) return fail(ctx, DSE_ERR_ARG, "null pointer");
+  HIPC(hipSetDevice(ctx->device));
+  int rc = prepare(ctx);
+  if (rc) return rc;
+  if ((rc = ensure_partial(ctx, 1))) return rc;
+  HostProblem& P = ctx->probs[problem];
+  hipStream_t st = ctx->lanes[0].stream;
+  const size_t bytes = (size_t(1) << P.n) * sizeof(double2);
+  HIPC(hipMemcpyAsync(P.buf[0], psi, bytes, hipMemcpyHostToDevice, st));
+  HIPC(launch_obs(P.L, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, ctx->d_partial, st));
+  std::vector<double> h(P.n_tiles * 8);
+  HIPC(hipMemcpyAsync(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int64_t t = 0; t < P.n_tiles; ++t)
+    for (int j = 0; j < 7; ++j) v[j] += h[t * 8 + j];
+  finish_obs(P, v, obs7, 1);
+  ctx->evolved = false;
+  return DSE_OK;
+}
+
+int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
+  if (!ctx) return DSE_ERR_ARG;
+  const auto wall0 = std::chrono::steady_clock::now();
+  if (!t || !obs_out) return fail(ctx, DSE_ERR_ARG, "null pointer");
+  if (n_t < 1) return fail(ctx, DSE_ERR_ARG, "n_t must be >= 1");
+  if (!(tol > 0.0 && tol < 1e-2)) return fail(ctx, DSE_ERR_ARG, "tol must be in (0, 1e-2)");
+  for (int i = 0; i < n_t; ++i)
+    if (!std::isfinite(t[i])) return fail(ctx, DSE_ERR_ARG, "non-finite time");
+  for (int i = 1; i < n_t; ++i)
+    if (!(t[i] > t[i - 1])) return fail(ctx, DSE_ERR_ARG, "times must be strictly increasing");
+  HIPC(hipSetDevice(ctx->device));
+  int rc = prepare(ctx);
+  if (rc) return rc;
+
+  // ---- distinct interval lengths -> coefficient sets ----
+  std::vector<double> set_dt;
+  std::vector<int> set_of(std::max(0, n_t - 1));
+  for (int m = 0; m + 1 < n_t; ++m) {
+    const double dt = t[m + 1] - t[m];
+    int s = -1;
+    for (size_t q = 0; q < set_dt.size(); ++q)
+      if (set_dt[q] == dt) {
+        s = (int)q;
+        break;
+      }
+    if (s < 0) {
+      if (set_dt.size() >= 4096) return fail(ctx, DSE_ERR_ARG, "more than 4096 distinct output intervals");
+      s = (int)set_dt.size();
+      set_dt.push_back(dt);
+    }
+    set_of[m] = s;
+  }
+  if (set_dt.empty()) set_dt.push_back(0.0);
+  const int n_sets = (int)set_dt.size();
+
+  // ---- Chebyshev coefficients per problem ----
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    HostProblem& P = ctx->probs[pi];
+    const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
+    const double beta = 0.5 * (P.e_max + P.e_min);
+    int deg = 1;
+    std::vector<std::vector<double>> J(n_sets);
+    for (int s = 0; s < n_sets; ++s) {
+      const double z = alpha * set_dt[s];
+      const int kmax = (int)std::ceil(z + 12.0 * std::cbrt(z + 1.0) + 60.0);
+      if (kmax > ctx->max_degree)
+        return fail(ctx, DSE_ERR_CONVERGENCE, "Chebyshev degree " + std::to_string(kmax) +
+                                                  " exceeds max_degree; use a finer output grid");
+      J[s].resize(kmax + 1);
+      int d = 1;
+      if (dse_bessel_j(z, kmax, J[s].data(), tol, &d) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
+      deg = std::max(deg, d);
+    }
+    P.degree = deg;
+    const int kcap1 = deg + 1;
+    std::vector<CoefK> coef((size_t)n_sets * kcap1);
+    std::memset(coef.data(), 0, coef.size() * sizeof(CoefK));
+    std::vector<std::complex<double>> a(deg + 1);
+    for (int s = 0; s < n_sets; ++s) {
+      const double ph = -beta * set_dt[s];
+      const std::complex<double> e(std::cos(ph), std::sin(ph));
+      std::complex<double> mi(1.0, 0.0);  // (-i)^k
+      for (int k = 0; k <= deg; ++k) {
+        const double jk = k < (int)J[s].size() ? J[s][k] : 0.0;
+        a[k] = e * mi * ((k == 0 ? 1.0 : 2.0) * jk);
+        mi *= std::complex<double>(0.0, -1.0);
+      }
+      auto put = [](double2& d, std::complex<double> v) { d = make_double2(v.real(), v.imag()); };
+      CoefK* row = coef.data() + (size_t)s * kcap1;
+      put(row[1].c[1], a[0]);  // k = 1: acc = a0 w0 + a1 w1
+      put(row[1].c[2], a[1]);
+      row[1].upd = 1;
+      for (int k = 2; k <= deg; ++k) {
+        const int r = (k - 1) % 3;  // regular update every third term covers k-2..k
+        const int nterm = (r == 0) ? 3 : (k == deg ? r : 0);
+        row[k].upd = nterm > 0;
+        if (nterm >= 3) put(row[k].c[0], a[k - 2]);
+        if (nterm >= 2) put(row[k].c[1], a[k - 1]);
+        if (nterm >= 1) put(row[k].c[2], a[k]);
+      }
+    }
+    const size_t cb = coef.size() * sizeof(CoefK);
+    if (cb > P.coef_bytes) {
+      if (P.coef) (void)hipFree(P.coef), P.coef = nullptr;
+      if (hipMalloc(&P.coef, cb) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed");
+      P.coef_bytes = cb;
+    }
+    HIPC(hipMemcpy(P.coef, coef.data(), cb, hipMemcpyHostToDevice));
+    DevProb& d = ctx->h_desc[pi];
+    d.coef = P.coef;
+    d.kcap1 = kcap1;
+    d.degree = deg;
+    d.beta = beta;
+    d.s1 = 1.0 / alpha;
+  }
+  HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
+
+  // ---- lanes: problems by degree (desc) dealt round-robin over the streams, grouped by tile ----
+  const int n_lanes = std::min<int>(ctx->n_streams, (int)ctx->probs.size());
+  std::vector<int> order(ctx->probs.size());
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return ctx->probs[a].degree > ctx->probs[b].degree;
+  });
+  std::vector<std::map<int, std::vector<int>>> lane_probs(n_lanes);  // lane -> L -> problems
+  for (size_t i = 0; i < order.size(); ++i) lane_probs[i % n_lanes][ctx->probs[order[i]].L].push_back(order[i]);
+  std::vector<int2> items;
+  items.reserve(ctx->total_items);
+  ctx->item_pos.assign(ctx->probs.size(), 0);
+  int max_deg = 1;
+  for (int li = 0; li < (int)ctx->lanes.size(); ++li) {
+    Lane& ln = ctx->lanes[li];
+    ln.groups.clear();
+    ln.max_deg = 0;
+    if (li >= n_lanes) continue;
+    for (auto& kv : lane_probs[li]) {
+      LaneGroup g;
+      g.L = kv.first;
+      g.off = (int64_t)items.size();
+      for (int pi : kv.second) {  // already in degree order
+        ctx->item_pos[pi] = (int64_t)items.size();
+        for (int64_t tt = 0; tt < ctx->probs[pi].n_tiles; ++tt) items.push_back(make_int2(pi, (int)tt));
+        ln.max_deg = std::max(ln.max_deg, ctx->probs[pi].degree);
+      }
+      g.count = (int64_t)items.size() - g.off;
+      const int gdeg = ctx->probs[kv.second.front()].degree;
+      g.active.assign(gdeg + 2, 0);
+      g.bytes.assign(gdeg + 2, 0.0);
+      const double T = (double)(int64_t(1) << g.L);
+      for (int k = 0; k <= gdeg + 1; ++k) {
+        int64_t c = 0;
+        double by = 0.0;
+        for (int pi : kv.second) {
+          const int K = ctx->probs[pi].degree;
+          if (K < k) continue;
+          c += ctx->probs[pi].n_tiles;
+          // read w_{k-1}, read+write w_{k-2}/w_k (48 B/amp), plus acc read+write on update terms
+          const bool upd = (k >= 2) && (((k - 1) % 3 == 0) || k == K);
+          by += (double)ctx->probs[pi].n_tiles * T * (upd ? 80.0 : 48.0);
+        }
+        g.active[k] = (int)c;
+        g.bytes[k] = by;
+      }
+      ln.groups.push_back(std::move(g));
+    }
+    max_deg = std::max(max_deg, ln.max_deg);
+  }
+  HIPC(hipMemcpy(ctx->d_items, items.data(), items.size() * sizeof(int2), hipMemcpyHostToDevice));
+
+  // ---- psi(t0) = |psi0> ----
+  hipStream_t st0 = ctx->lanes[0].stream;
+  for (auto& P : ctx->probs) {
+    const size_t vbytes = (size_t(1) << P.n) * sizeof(double2);
+    HIPC(hipMemsetAsync(P.buf[0], 0, vbytes, st0));
+    static const double2 one = {1.0, 0.0};
+    HIPC(hipMemcpyAsync(P.buf[0] + P.psi0, &one, sizeof(double2), hipMemcpyHostToDevice, st0));
+  }
+  HIPC(hipStreamSynchronize(st0));
+
+  const size_t chunk = (size_t)std::min<int64_t>(
+      n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64)));
+  if ((rc = ensure_partial(ctx, chunk))) return rc;
+  if (ctx->time_every > 0)
+    for (auto& ln : ctx->lanes)
+      if ((rc = ensure_events(ctx, ln, (size_t)ln.groups.size() * (ln.max_deg + 1) + 1))) return rc;
+
+  double step_ms = 0.0, launches_timed = 0.0, bytes_timed = 0.0;
+  double launches = 0.0, amp_updates = 0.0, all_bytes = 0.0;
+  std::vector<std::vector<double>> pool_bytes(ctx->lanes.size() * 2);
+  auto drain = [&](Lane& ln, size_t li, int pool) -> int {
+    if (ln.ev_used[pool] == 0) return DSE_OK;
+    HIPC(hipEventSynchronize(ln.ev[pool][2 * ln.ev_used[pool] - 1]));
+    for (size_t i = 0; i < ln.ev_used[pool]; ++i) {
+      float ms = 0.f;
+      HIPC(hipEventElapsedTime(&ms, ln.ev[pool][2 * i], ln.ev[pool][2 * i + 1]));
+      step_ms += ms;
+      bytes_timed += pool_bytes[li * 2 + pool][i];
+    }
+    launches_timed += (double)ln.ev_used[pool];
+    ln.ev_used[pool] = 0;
+    pool_bytes[li * 2 + pool].clear();
+    return DSE_OK;
+  };
+  auto obs_all = [&](int bsel_q, size_t slot) -> int {
+    for (auto& ln : ctx->lanes)
+      for (auto& g : ln.groups) {
+        const int bsel = bsel_q;
+        HIPC(launch_obs(g.L, ctx->d_probs, ctx->d_items + g.off, (int)g.count, bsel,
+                        ctx->d_partial + (slot * ctx->total_items + g.off) * 8, ln.stream));
+      }
+    return DSE_OK;
+  };
+
+  size_t slot = 0, t_flushed = 0;
+  if ((rc = obs_all(0, slot++))) return rc;
+  for (int m = 0; m + 1 < n_t; ++m) {
+    const int q = m & 1;
+    const int set = set_of[m];
+    const bool timed = ctx->time_every > 0 && (m % ctx->time_every) == 0;
+    const int pool = m & 1;
+    for (size_t li = 0; li < ctx->lanes.size(); ++li) {
+      Lane& ln = ctx->lanes[li];
+      if (ln.groups.empty()) continue;
+      if ((rc = drain(ln, li, pool))) return rc;
+      for (auto& g : ln.groups) {
+        const int T = 1 << g.L;
+        HIPC(launch_step(g.L, MODE_FIRST, ctx->d_probs, ctx->d_items + g.off, g.active[1], 1, q, set, ln.stream));
+        for (int k = 2; k < (int)g.active.size(); ++k) {
+          const int na = g.active[k];
+          if (na <= 0) break;
+          if (timed) {
+            const size_t i = ln.ev_used[pool]++;
+            HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
+            HIPC(launch_step(g.L, MODE_GEN, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
+            HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
+            pool_bytes[li * 2 + pool].push_back(g.bytes[k]);
+          } else {
+            HIPC(launch_step(g.L, MODE_GEN, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
+          }
+          launches += 1.0;
+          amp_updates += (double)na * T;
+          all_bytes += g.bytes[k];
+        }
+      }
+    }
+    // new psi of every problem sits in acc(q) = buf[q ? 0 : 2]
+    if ((rc = obs_all(q ? 0 : 2, slot++))) return rc;
+    if (slot == chunk) {
+      if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out))) return rc;
+      t_flushed += slot;
+      slot = 0;
+    }
+  }
+  if (slot > 0) {
+    if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out))) return rc;
+    t_flushed += slot;
+  }
+  for (size_t li = 0; li < ctx->lanes.size(); ++li)
+    for (int pool = 0; pool < 2; ++pool)
+      if ((rc = drain(ctx->lanes[li], li, pool))) return rc;
+  if ((rc = sync_all(ctx))) return rc;
+  ctx->last_q = (n_t - 1) & 1;
+  ctx->evolved = true;
+
+  if (stats) {
+    double happl = 0.0;
+    for (auto& P : ctx->probs) happl += (double)P.degree * (n_t - 1);
+    std::memset(stats, 0, sizeof(*stats));
+    stats->h_applications = happl;
+    stats->amplitude_updates = amp_updates;
+    stats->step_bytes = all_bytes;
+    stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
+    stats->step_launches = launches;
+    stats->timed_launches = launches_timed;
+    stats->timed_bytes = bytes_timed;
+    stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+    stats->max_degree = max_deg;
+    stats->n_intervals = n_t - 1;
+    stats->tile_bits = ctx->probs.empty() ? 0 : ctx->probs.front().L;
+    stats->streams = n_lanes;
+  }
+  return DSE_OK;
+}
+
+int dse_get_state(dse_ctx* ctx, int problem, double* psi_out) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (problem < 0 || problem >= (int)ctx->probs.size()) return fail(ctx, DSE_ERR_ARG, "bad problem id");
+  if (!psi_out) return fail(ctx, DSE_ERR_ARG, "null state");
+  if (!ctx->evolved) return fail(ctx, DSE_ERR_STATE, "no evolved state (call dse_evolve first)");
+  HIPC(hipSetDevice(ctx->device));
+  HostProblem& P = ctx->probs[problem];
+  const int bsel = ctx->last_q ? 2 : 0;
+  const size_t bytes = (size_t(1) << P.n) * sizeof(double2);
+  HIPC(hipMemcpy(psi_out, P.buf[bsel], bytes, hipMemcpyDeviceToHost));
+  return DSE_OK;
+}
+
+int dse_time_step_kernel(dse_ctx* ctx, int reps, double* ms_per_launch, double* bytes_per_launch) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (reps < 1 || !ms_per_launch || !bytes_per_launch) return fail(ctx, DSE_ERR_ARG, "bad arguments");
+  if (!ctx->evolved) return fail(ctx, DSE_ERR_STATE, "call dse_evolve first (coefficients needed)");
+  HIPC(hipSetDevice(ctx->device));
+  Lane& ln = ctx->lanes[0];
+  int rc = ensure_events(ctx, ln, (size_t)reps);
+  if (rc) return rc;
+  // one launch over every item of every lane: the whole batch at term k = 2
+  std::vector<int2> items(ctx->total_items);
+  HIPC(hipMemcpy(items.data(), ctx->d_items, items.size() * sizeof(int2), hipMemcpyDeviceToHost));
+  std::map<int, std::vector<int2>> by_L;
+  for (auto& it : items) by_L[ctx->probs[it.x].L].push_back(it);
+  int2* d_tmp = nullptr;
+  HIPC(hipMalloc(&d_tmp, items.size() * sizeof(int2)));
+  double bytes = 0.0, tot = 0.0;
+  int64_t off = 0;
+  std::vector<std::pair<int, int64_t>> segs;
+  for (auto& kv : by_L) {
+    HIPC(hipMemcpy(d_tmp + off, kv.second.data(), kv.second.size() * sizeof(int2), hipMemcpyHostToDevice));
+    segs.push_back({kv.first, off});
+    off += (int64_t)kv.second.size();
+    bytes += 48.0 * (double)kv.second.size() * (double)(1 << kv.first);
+  }
+  for (int r = 0; r < reps; ++r) {
+    HIPC(hipEventRecord(ln.ev[0][2 * r], ln.stream));
+    for (size_t s = 0; s < segs.size(); ++s) {
+      const int64_t cnt = (s + 1 < segs.size() ? segs[s + 1].second : off) - segs[s].second;
+      HIPC(launch_step(segs[s].first, MODE_GEN, ctx->d_probs, d_tmp + segs[s].second, (int)cnt, 2, 0, 0, ln.stream));
+    }
+    HIPC(hipEventRecord(ln.ev[0][2 * r + 1], ln.stream));
+  }
+  HIPC(hipStreamSynchronize(ln.stream));
+  for (int r = 0; r < reps; ++r) {
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ln.ev[0][2 * r], ln.ev[0][2 * r + 1]));
+    tot += ms;
+  }
+  (void)hipFree(d_tmp);
+  *ms_per_launch = tot / reps;
+  *bytes_per_launch = bytes;
+  ctx->evolved = false;  // buffers now hold timing garbage
+  return DSE_OK;
+}
+
+}  // extern "C"

@@ -75,7 +75,7 @@ def test_apply_h_matches_reference_n12(engine, golden, variant, tile_bits):
         pid = engine.add(prob)
         out = engine.apply_h(pid, g[f"{variant}_v"])
     finally:
-        engine.set_option("tile_bits", 12)
+        engine.set_option("tile_bits", 13)
     ref = g[f"{variant}_Hv"]
     assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
 
@@ -92,7 +92,7 @@ def test_apply_h_random_tables(engine, n, tile_bits):
         v = _rand(n, n)
         out = engine.apply_h(pid, v)
     finally:
-        engine.set_option("tile_bits", 12)
+        engine.set_option("tile_bits", 13)
     ref = rm.bitwise_apply(_tables(prob), v)
     assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
 
@@ -121,7 +121,7 @@ def test_observables_random(engine, n, tile_bits):
         v = _rand(n, 3 * n) * 1.7
         o = engine.observables(pid, v)
     finally:
-        engine.set_option("tile_bits", 12)
+        engine.set_option("tile_bits", 13)
     ref = rm.observables_bitwise(v, n, prob.sea_mask, prob.rare_bit)
     np.testing.assert_allclose(o, ref, rtol=0, atol=1e-12)
 
@@ -163,19 +163,28 @@ def test_evolve_tile_size_and_batch_invariance(engine):
     t = np.linspace(0.0, 2e-5, 5)
     params = [sweep_point_params(13, d, v, 2e-5, 5) for d in (0.0, 150000.0) for v in VARIANTS]
     res = {}
-    for tb in (12, 13):
+    for tb in (13, 12):
         engine.clear()
         engine.set_option("tile_bits", tb)
         for p in params:
             engine.add(pb.build_problem(p))
         res[tb], _ = engine.evolve(t)
-    engine.set_option("tile_bits", 12)
+    engine.set_option("tile_bits", 13)
     np.testing.assert_allclose(res[12], res[13], rtol=0, atol=1e-11)
     engine.clear()
     engine.add(pb.build_problem(params[4]))
     single, _ = engine.evolve(t)
     np.testing.assert_allclose(single[0], res[12][4], rtol=0, atol=1e-12)
     np.testing.assert_allclose(res[12][:, 6], 1.0, atol=1e-11)
+    for ns in (1, 3):
+        engine.clear()
+        engine.set_option("streams", ns)
+        for p in params:
+            engine.add(pb.build_problem(p))
+        got, st = engine.evolve(t)
+        assert st["streams"] == min(ns, len(params))
+        np.testing.assert_allclose(got, res[13], rtol=0, atol=1e-12)
+    engine.set_option("streams", 4)
 
 
 def test_evolve_nonuniform_grid_and_single_point(engine):
