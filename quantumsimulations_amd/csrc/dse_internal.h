@@ -13,6 +13,8 @@ constexpr int kMinTile = 1;
 constexpr int kMaxTile = 13;
 constexpr int kRegBlockMinTile = 9;  // tiles >= 2^9 use the register-block kernel
 constexpr int kRegBits = 3;          // amplitudes per thread = 2^kRegBits in that kernel
+// bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index
+#define DSE_MAX_HIGH_BITS(L) ((34 - (L)) < 0 ? 0 : (34 - (L)))
 
 // A pair flip or a drive flip, split into its in-tile mask and its tile-index mask.
 //   pair : applies iff bit_i(x) == bit_j(x) <=> popc(x_lo & mask_lo) + popc(h & tile_xor) even
@@ -79,6 +81,7 @@ struct DevProb {
 
 hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items, int n_items,
                        int k, int q, int set, hipStream_t st);
+hipError_t set_ablate(int mask);
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
                       double* partial, hipStream_t st);
 

@@ -15,6 +15,14 @@
 #include "dse_internal.h"
 
 namespace dse {
+
+// Diagnostic ablation mask (0 in production): sections of k_step_rb to skip, for timing only.
+//   1 thread-bit sweeps   2 thread-thread pairs   4 cross-tile terms   8 epilogue global reads
+//   16 diagonal table read   32 tile load from global memory
+__device__ int g_dse_ablate = 0;
+
+hipError_t set_ablate(int mask) { return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_ablate), &mask, sizeof(int)); }
+
 namespace {
 
 template <int L>
@@ -34,37 +42,65 @@ __device__ __forceinline__ double2 cmad(double2 acc, double cr, double ci, doubl
 
 __device__ __forceinline__ int par32(uint32_t v) { return __popc(v) & 1; }
 
+// Global address-space views: loads through them are global_load (vmcnt only) instead of
+// flat_load (which also counts against lgkmcnt and serialises LDS work).
+typedef double __attribute__((ext_vector_type(2))) dv2;
+typedef __attribute__((address_space(1))) dv2 gd2;
+typedef __attribute__((address_space(1))) double gdbl;
+__device__ __forceinline__ gd2* gptr(double2* p) { return (gd2*)p; }
+__device__ __forceinline__ const gdbl* gptr(const double* p) { return (const gdbl*)p; }
+__device__ __forceinline__ double2 gld(const gd2* p, size_t i) {
+  const dv2 v = p[i];
+  return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void gst(gd2* p, size_t i, double2 a) {
+  dv2 v;
+  v.x = a.x;
+  v.y = a.y;
+  p[i] = v;
+}
+
+// Cooperative copy of n16 16-byte granules from global memory into LDS.
+__device__ __forceinline__ void stage16(void* dst, const void* src, int n16, int tid, int nt) {
+  const gd2* s = (const gd2*)src;
+  dv2* d = (dv2*)dst;
+  for (int i = tid; i < n16; i += nt) d[i] = s[i];
+}
+
 // Recurrence + propagator accumulation for one amplitude (see CoefK):
 //   MODE_APPLY  wdst = H w
 //   MODE_FIRST  w1 = s1 * (H - beta) w0,  acc = c1 w0 + c2 w1
 //   MODE_GEN    w_k = s2 * (H - beta) w_{k-1} - w_{k-2} (in place),  acc += c0 w_{k-2} + c1 w_{k-1} + c2 w_k
-template <int MODE>
+__device__ __forceinline__ double2 gld(const double2* p, size_t i) { return p[i]; }
+__device__ __forceinline__ void gst(double2* p, size_t i, double2 a) { p[i] = a; }
+
+template <int MODE, typename Ptr>
 __device__ __forceinline__ void step_epilogue(size_t x, double2 out, double2 own, double scale,
-                                              double2* __restrict__ wdst, double2* __restrict__ acc_b,
-                                              const CoefK& C) {
+                                              Ptr __restrict__ wdst, Ptr __restrict__ acc_b,
+                                              const CoefK& C, int no_reads) {
   if (MODE == MODE_APPLY) {
-    wdst[x] = out;
+    gst(wdst, x, out);
   } else if (MODE == MODE_FIRST) {
     double2 w;
     w.x = scale * out.x;
     w.y = scale * out.y;
-    wdst[x] = w;
+    gst(wdst, x, w);
     double2 a = make_double2(0.0, 0.0);
     a = cmad(a, C.c[1].x, C.c[1].y, own);
     a = cmad(a, C.c[2].x, C.c[2].y, w);
-    acc_b[x] = a;
+    gst(acc_b, x, a);
   } else {
-    const double2 prev = wdst[x];
+    const double2 prev = no_reads ? make_double2(0.0, 0.0) : gld(wdst, x);
     double2 w;
     w.x = fma(scale, out.x, -prev.x);
     w.y = fma(scale, out.y, -prev.y);
-    wdst[x] = w;
+    gst(wdst, x, w);
     if (C.upd) {
-      double2 a = acc_b[x];
+      double2 a = no_reads ? make_double2(0.0, 0.0) : gld(acc_b, x);
       a = cmad(a, C.c[0].x, C.c[0].y, prev);
       a = cmad(a, C.c[1].x, C.c[1].y, own);
       a = cmad(a, C.c[2].x, C.c[2].y, w);
-      acc_b[x] = a;
+      gst(acc_b, x, a);
     }
   }
 }
@@ -220,7 +256,7 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
   const double scale = MODE == MODE_GEN ? 2.0 * P.s1 : P.s1;
 #pragma unroll
   for (int r = 0; r < R; ++r)
-    step_epilogue<MODE>(base + r * NT + tid, out[r], own[r], scale, wdst, acc_b, C);
+    step_epilogue<MODE>(base + r * NT + tid, out[r], own[r], scale, wdst, acc_b, C, 0);
 }
 
 // Observables of one state: per tile partial sums of
@@ -337,12 +373,27 @@ struct RB {
   static constexpr int TB = L - kRegBits;    // tile bits carried by the thread index
 };
 
+// Upper bounds of the cross-tile term lists for a 34-qubit register (static LDS staging).
+template <int L>
+struct HiCap {
+  static constexpr int HB = DSE_MAX_HIGH_BITS(L);
+  static constexpr int PAIRS = HB * L + HB * (HB - 1) / 2 + 1;
+  static constexpr int FLIPS = HB + 1;
+};
+
 template <int L, int MODE>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int k, int q, int set) {
   constexpr int NT = RB<L>::NT, TB = RB<L>::TB;
+  constexpr int NTT = TB * (TB - 1) / 2;
   __shared__ double2 s_w[RB<L>::T];
   __shared__ double s_c[L + 1];
+  // per-problem term tables, staged once per workgroup (vector loads of generic pointers inside
+  // the loops would serialise every iteration behind a global-memory round trip)
+  __shared__ DSweep s_sw[TB];
+  __shared__ DPair s_tt[NTT > 0 ? NTT : 1];
+  __shared__ DPair s_ph[HiCap<L>::PAIRS];
+  __shared__ DFlip s_fh[HiCap<L>::FLIPS];
 
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
@@ -350,14 +401,16 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   const int tid = threadIdx.x;
   if (MODE == MODE_GEN && k > P.degree) return;  // uniform: this problem's interval is done
 
-  double2* psi_b = P.buf[q ? 2 : 0];
-  double2* acc_b = P.buf[q ? 0 : 2];
-  double2* scr_b = P.buf[1];
-  const double2* win;
-  double2* wdst;
+  const int ab = g_dse_ablate;
+  const int n_tt = P.n_pairs_tt, n_ph = P.n_pairs_hi, n_fh = P.n_flips_hi;
+  gd2* psi_b = gptr(P.buf[q ? 2 : 0]);
+  gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
+  gd2* scr_b = gptr(P.buf[1]);
+  const gd2* win;
+  gd2* wdst;
   if (MODE == MODE_APPLY) {
-    win = P.buf[0];
-    wdst = P.buf[1];
+    win = gptr(P.buf[0]);
+    wdst = gptr(P.buf[1]);
   } else if (MODE == MODE_FIRST) {
     win = psi_b;
     wdst = scr_b;
@@ -367,72 +420,89 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   }
   const size_t base = (size_t)h << L;
 
-  double2 own[8];
+  stage16(s_sw, P.sweeps, TB * (int)(sizeof(DSweep) / 16), tid, NT);
+  stage16(s_tt, P.pairs_tt, n_tt, tid, NT);
+  stage16(s_ph, P.pairs_hi, n_ph, tid, NT);
+  stage16(s_fh, P.flips_hi, n_fh * (int)(sizeof(DFlip) / 16), tid, NT);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    own[r] = win[base + r * NT + tid];
-    s_w[r * NT + tid] = own[r];
-  }
+  for (int r = 0; r < 8; ++r)
+    s_w[r * NT + tid] = (ab & 32) ? make_double2(1.0, 0.0) : gld(win, base + r * NT + tid);
   tile_diag_coeffs<L>(P, h, MODE == MODE_APPLY ? 0.0 : P.beta, s_c, tid);
+  const gdbl* zzlo = gptr(P.zzlo);
+  double zd[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) zd[r] = (ab & 16) ? 0.0 : zzlo[r * NT + tid];
   __syncthreads();
 
-  // ---- diagonal ----
-  double gt = s_c[L];
+  // The first cross-tile flip (the rare drive in the center geometry) reads the partner tile
+  // elementwise: issue those loads now so their latency hides under the LDS work below.
+  const bool pre = (n_fh > 0) && !(ab & 4);
+  double2 part[8];
+  if (pre) {
+    const DFlip F = s_fh[0];
+    const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
 #pragma unroll
-  for (int i = 0; i < TB; ++i) gt += s_c[i] * (0.5 - (double)((tid >> i) & 1));
-  const double fa = 0.5 * s_c[TB], fb = 0.5 * s_c[TB + 1], fc = 0.5 * s_c[TB + 2];
-  double2 out[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const double d = P.zzlo[r * NT + tid] + gt + ((r & 1) ? -fa : fa) + ((r & 2) ? -fb : fb) +
-                     ((r & 4) ? -fc : fc);
-    out[r].x = d * own[r].x;
-    out[r].y = d * own[r].y;
+    for (int r = 0; r < 8; ++r) part[r] = gld(src, (uint32_t)(r * NT + tid) ^ F.mask_lo);
   }
 
-  // ---- register bits: drive flips and pair flips need no memory ----
-  if (P.rflip_mask) {
+  // ---- diagonal + register-bit terms (own amplitudes) ----
+  double2 out[8];
+  {
+    double2 own[8];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (!((P.rflip_mask >> i) & 1)) continue;
-      const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
+    for (int r = 0; r < 8; ++r) own[r] = s_w[r * NT + tid];
+    double gt = s_c[L];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const bool v = (r >> i) & 1;
-        out[r] = cmad(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
-      }
-    }
-  }
-#pragma unroll
-  for (int pp = 0; pp < 3; ++pp) {
-    const int a = (pp == 2) ? 1 : 0, b = (pp == 0) ? 1 : 2;
-    const double g = P.rr_g[pp];
-    if (g == 0.0) continue;
+    for (int i = 0; i < TB; ++i) gt += s_c[i] * (0.5 - (double)((tid >> i) & 1));
+    const double fa = 0.5 * s_c[TB], fb = 0.5 * s_c[TB + 1], fc = 0.5 * s_c[TB + 2];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
-      const double2 s = own[r ^ ((1 << a) | (1 << b))];
-      out[r].x = fma(g, s.x, out[r].x);
-      out[r].y = fma(g, s.y, out[r].y);
+      const double d = zd[r] + gt + ((r & 1) ? -fa : fa) + ((r & 2) ? -fb : fb) + ((r & 4) ? -fc : fc);
+      out[r].x = d * own[r].x;
+      out[r].y = d * own[r].y;
+    }
+    if (P.rflip_mask) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (!((P.rflip_mask >> i) & 1)) continue;
+        const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const bool v = (r >> i) & 1;
+          out[r] = cmad(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
+        }
+      }
+    }
+#pragma unroll
+    for (int pp = 0; pp < 3; ++pp) {
+      const int a = (pp == 2) ? 1 : 0, b = (pp == 0) ? 1 : 2;
+      const double g = P.rr_g[pp];
+      if (g == 0.0) continue;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
+        const double2 sv = own[r ^ ((1 << a) | (1 << b))];
+        out[r].x = fma(g, sv.x, out[r].x);
+        out[r].y = fma(g, sv.y, out[r].y);
+      }
     }
   }
 
   // ---- thread bits: one LDS sweep of the partner thread per bit j ----
-  for (int j = 0; j < TB; ++j) {
-    const DSweep& S = P.sweeps[j];
-    const uint32_t hf = S.has_flip, hp = S.has_pair;
-    if (!(hf | hp)) continue;
+  for (int j = 0; j < ((ab & 1) ? 0 : TB); ++j) {
+    const DSweep S = s_sw[j];
+    if (!(S.has_flip | S.has_pair)) continue;
     const int bj = (tid >> j) & 1;
     const int pt = tid ^ (1 << j);
     double2 pv[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) pv[r] = s_w[r * NT + pt];
-    if (hf) {
+    if (S.has_flip) {
       const double cr = bj ? S.re1 : S.re0, ci = bj ? S.im1 : S.im0;
 #pragma unroll
       for (int r = 0; r < 8; ++r) out[r] = cmad(out[r], cr, ci, pv[r]);
     }
-    if (hp) {
+    if (S.has_pair) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const double g = S.g[i];
@@ -440,72 +510,119 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const double gg = ((r >> i) & 1) ? g1 : g0;
-          const double2 s = pv[r ^ (1 << i)];
-          out[r].x = fma(gg, s.x, out[r].x);
-          out[r].y = fma(gg, s.y, out[r].y);
+          const double2 sv = pv[r ^ (1 << i)];
+          out[r].x = fma(gg, sv.x, out[r].x);
+          out[r].y = fma(gg, sv.y, out[r].y);
         }
       }
     }
   }
+  // ---- the prefetched first cross-tile flip (loads issued before the sweeps) ----
+  if (pre) {
+    const DFlip F = s_fh[0];
+    const bool v = par32(h & F.tile_xor);
+    const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) out[r] = cmad(out[r], cr, ci, part[r]);
+  }
+  // ---- epilogue operand w_{k-2}: issued now, its latency hides under the pair loop ----
+  CoefK C = {};
+  if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
+  const bool rd = (MODE == MODE_GEN) && !(ab & 8);
+  double2 prev[8];
+  if (rd) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) prev[r] = gld(wdst, base + r * NT + tid);
+  }
+
   // ---- pairs between two thread bits ----
-  for (int p = 0; p < P.n_pairs_tt; ++p) {
-    const DPair Q = P.pairs_tt[p];
+  for (int p = 0; p < ((ab & 2) ? 0 : n_tt); ++p) {
+    const DPair Q = s_tt[p];
     if (__popc((uint32_t)tid & Q.mask_lo) & 1) continue;
     const int pt = tid ^ (int)Q.mask_lo;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const double2 s = s_w[r * NT + pt];
-      out[r].x = fma(Q.g, s.x, out[r].x);
-      out[r].y = fma(Q.g, s.y, out[r].y);
+      const double2 sv = s_w[r * NT + pt];
+      out[r].x = fma(Q.g, sv.x, out[r].x);
+      out[r].y = fma(Q.g, sv.y, out[r].y);
     }
   }
 
   // ---- terms reaching other tiles (global, L2/MALL-served) ----
-  for (int f = 0; f < P.n_flips_hi; ++f) {
-    const DFlip F = P.flips_hi[f];
+  // (processed four registers at a time to bound register pressure)
+  for (int f = 1; f < ((ab & 4) ? 0 : n_fh); ++f) {
+    const DFlip F = s_fh[f];
     const bool v = par32(h & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
-    const double2* src = win + ((size_t)(h ^ F.tile_xor) << L);
+    const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const uint32_t x = (uint32_t)(r * NT + tid);
-      out[r] = cmad(out[r], cr, ci, src[x ^ F.mask_lo]);
+    for (int hr = 0; hr < 8; hr += 4) {
+      double2 sv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr + r) * NT + tid) ^ F.mask_lo);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[hr + r] = cmad(out[hr + r], cr, ci, sv[r]);
     }
   }
-  for (int p = 0; p < P.n_pairs_hi; ++p) {
-    const DPair Q = P.pairs_hi[p];
+  for (int p = 0; p < ((ab & 4) ? 0 : n_ph); ++p) {
+    const DPair Q = s_ph[p];
     const int hpar = par32(h & Q.tile_xor);
-    const double2* src = win + ((size_t)(h ^ Q.tile_xor) << L);
-    if (Q.mask_lo == 0u) {
-      if (hpar) continue;
+    if (Q.mask_lo == 0u && hpar) continue;  // both bits above the tile: uniform condition
+    const gd2* src = win + ((size_t)(h ^ Q.tile_xor) << L);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const double2 s = src[r * NT + tid];
-        out[r].x = fma(Q.g, s.x, out[r].x);
-        out[r].y = fma(Q.g, s.y, out[r].y);
-      }
-    } else {
+    for (int hr = 0; hr < 8; hr += 4) {
+      double2 sv[4];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t x = (uint32_t)(r * NT + tid);
-        if (!((__popc(x & Q.mask_lo) + hpar) & 1)) {
-          const double2 s = src[x ^ Q.mask_lo];
-          out[r].x = fma(Q.g, s.x, out[r].x);
-          out[r].y = fma(Q.g, s.y, out[r].y);
-        }
+      for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr + r) * NT + tid) ^ Q.mask_lo);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t x = (uint32_t)((hr + r) * NT + tid);
+        const double g = ((__popc(x & Q.mask_lo) + hpar) & 1) ? 0.0 : Q.g;
+        out[hr + r].x = fma(g, sv[r].x, out[hr + r].x);
+        out[hr + r].y = fma(g, sv[r].y, out[hr + r].y);
       }
     }
   }
 
   // ---- recurrence + accumulation ----
-  CoefK C = {};
-  if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
+  const bool rd_acc = rd && C.upd;
+  double2 accv[8];
+  if (rd_acc) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) accv[r] = gld(acc_b, base + r * NT + tid);
+  }
   const double scale = MODE == MODE_GEN ? 2.0 * P.s1 : P.s1;
 #pragma unroll
-  for (int r = 0; r < 8; ++r)
-    step_epilogue<MODE>(base + r * NT + tid, out[r], own[r], scale, wdst, acc_b, C);
+  for (int r = 0; r < 8; ++r) {
+    const size_t x = base + r * NT + tid;
+    const double2 own = s_w[r * NT + tid];
+    if (MODE == MODE_APPLY) {
+      gst(wdst, x, out[r]);
+    } else if (MODE == MODE_FIRST) {
+      double2 w;
+      w.x = scale * out[r].x;
+      w.y = scale * out[r].y;
+      gst(wdst, x, w);
+      double2 a = make_double2(0.0, 0.0);
+      a = cmad(a, C.c[1].x, C.c[1].y, own);
+      a = cmad(a, C.c[2].x, C.c[2].y, w);
+      gst(acc_b, x, a);
+    } else {
+      const double2 pr = rd ? prev[r] : make_double2(0.0, 0.0);
+      double2 w;
+      w.x = fma(scale, out[r].x, -pr.x);
+      w.y = fma(scale, out[r].y, -pr.y);
+      gst(wdst, x, w);
+      if (C.upd) {
+        double2 a = rd_acc ? accv[r] : make_double2(0.0, 0.0);
+        a = cmad(a, C.c[0].x, C.c[0].y, pr);
+        a = cmad(a, C.c[1].x, C.c[1].y, own);
+        a = cmad(a, C.c[2].x, C.c[2].y, w);
+        gst(acc_b, x, a);
+      }
+    }
+  }
 }
-
 
 // ------------------------------------------------------------------------------------------
 // launch dispatch over the tile size

@@ -86,6 +86,7 @@ struct dse_ctx {
   int last_q = 0;
   int tile_bits = 13;
   int n_streams = 4;
+  int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
   double max_degree = 2e6;
 };
@@ -455,6 +456,10 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "time_kernels") {
     if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
     ctx->time_every = (int)value;
+  } else if (k == "ablate") {  // diagnostics only: skip kernel sections (results become wrong)
+    HIPC(set_ablate((int)value));
+  } else if (k == "probe_items") {  // diagnostics only: dse_time_step_kernel launches this many items
+    ctx->probe_items = (int64_t)value;
   } else if (k == "max_degree") {
     if (!(value >= 1)) return fail(ctx, DSE_ERR_ARG, "max_degree must be >= 1");
     ctx->max_degree = value;
@@ -850,6 +855,7 @@ int dse_time_step_kernel(dse_ctx* ctx, int reps, double* ms_per_launch, double* 
   std::vector<int2> items(ctx->total_items);
   HIPC(hipMemcpy(items.data(), ctx->d_items, items.size() * sizeof(int2), hipMemcpyDeviceToHost));
   std::map<int, std::vector<int2>> by_L;
+  if (ctx->probe_items > 0 && (int64_t)items.size() > ctx->probe_items) items.resize(ctx->probe_items);
   for (auto& it : items) by_L[ctx->probs[it.x].L].push_back(it);
   int2* d_tmp = nullptr;
   HIPC(hipMalloc(&d_tmp, items.size() * sizeof(int2)));
