@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 1
+#define DSE_ABI_VERSION 2
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -69,15 +69,21 @@ typedef struct dse_stats {
   double h_applications;      /* Chebyshev terms = applications of H, summed over problems     */
   double amplitude_updates;   /* sum over step launches of the amplitudes they updated          */
   double step_bytes;          /* algorithmic HBM bytes of all step launches (80 B / amplitude)  */
-  double step_kernel_ms;      /* summed HIP-event time of the timed step launches (-1: none)    */
-  double step_launches;       /* number of step kernel launches (k >= 2)                        */
-  double timed_launches;      /* step launches bracketed by HIP events                          */
+  double step_kernel_ms;      /* summed HIP-event time of the timed launches of the dominant    */
+                              /* kernel (streaming: k_step_rb, k >= 2; persistent: k_interval)  */
+  double step_launches;       /* launches of the dominant kernel                                */
+  double timed_launches;      /* dominant-kernel launches bracketed by HIP events               */
   double timed_bytes;         /* algorithmic bytes of the timed launches                        */
   double wall_ms;             /* host wall time of the call                                     */
+  double h_flops;             /* algorithmic flops of all H applications (4 + 8/drive + 2/pair  */
+                              /* per amplitude)                                                 */
+  double timed_flops;         /* algorithmic flops of the timed launches                        */
   int32_t max_degree;         /* largest Chebyshev degree of any problem / interval             */
   int32_t n_intervals;        /* output intervals propagated                                    */
   int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
   int32_t streams;            /* HIP streams ("lanes") the problems were spread over            */
+  int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel   */
+  int32_t reserved;
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -101,6 +107,9 @@ void dse_destroy(dse_ctx* ctx);
 const char* dse_last_error(const dse_ctx* ctx);
 /* Options: "tile_bits"    LDS tile, log2 amplitudes per workgroup, 1..13 (default 13)
  *          "streams"      HIP streams the problems are spread over, 1..16 (default 4)
+ *          "persistent"   1 (default): one persistent launch per output interval when every
+ *                         problem fits one or two LDS tiles (n <= tile_bits + 1); 0: per-term
+ *                         streaming launches
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
  *          "max_degree"   Chebyshev degree cap per interval (default 2e6) */

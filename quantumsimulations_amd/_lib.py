@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 1
+DSE_ABI_VERSION = 2
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -40,10 +40,14 @@ class DseStats(C.Structure):
         ("timed_launches", C.c_double),
         ("timed_bytes", C.c_double),
         ("wall_ms", C.c_double),
+        ("h_flops", C.c_double),
+        ("timed_flops", C.c_double),
         ("max_degree", C.c_int32),
         ("n_intervals", C.c_int32),
         ("tile_bits", C.c_int32),
         ("streams", C.c_int32),
+        ("mode", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
     def as_dict(self):

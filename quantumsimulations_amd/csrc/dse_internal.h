@@ -82,6 +82,10 @@ struct DevProb {
 hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items, int n_items,
                        int k, int q, int set, hipStream_t st);
 hipError_t set_ablate(int mask);
+hipError_t set_ablate_interval(int mask);
+bool interval_supported(int L);
+hipError_t launch_interval(int L, const DevProb* probs, const int2* items, int n_items, int q,
+                           int set, int* flags, int* err, hipStream_t st);
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
                       double* partial, hipStream_t st);
 

@@ -12,7 +12,7 @@
 // MODE_APPLY: out = H w (test hook)      MODE_FIRST: w1 = Ht w0,  acc = a0 w0 + a1 w1
 // MODE_GEN:   w_k = 2 Ht w_{k-1} - w_{k-2} (in place over w_{k-2}),  acc += a_k w_k
 // with Ht = (H - beta) / alpha.
-#include "dse_internal.h"
+#include "dse_device.h"
 
 namespace dse {
 
@@ -24,109 +24,6 @@ __device__ int g_dse_ablate = 0;
 hipError_t set_ablate(int mask) { return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_ablate), &mask, sizeof(int)); }
 
 namespace {
-
-template <int L>
-struct Geo {
-  static constexpr int T = 1 << L;
-  static constexpr int NT = (L >= 13) ? 512 : (T >= 256 ? 256 : 64);
-  static constexpr int LGNT = (L >= 13) ? 9 : (T >= 256 ? 8 : 6);
-  static constexpr int R = (T >= NT) ? T / NT : 1;
-  static constexpr int TB = (L < LGNT) ? L : LGNT;  // tile bits carried by the thread index
-};
-
-__device__ __forceinline__ double2 cmad(double2 acc, double cr, double ci, double2 s) {
-  acc.x = fma(cr, s.x, fma(-ci, s.y, acc.x));
-  acc.y = fma(cr, s.y, fma(ci, s.x, acc.y));
-  return acc;
-}
-
-__device__ __forceinline__ int par32(uint32_t v) { return __popc(v) & 1; }
-
-// Global address-space views: loads through them are global_load (vmcnt only) instead of
-// flat_load (which also counts against lgkmcnt and serialises LDS work).
-typedef double __attribute__((ext_vector_type(2))) dv2;
-typedef __attribute__((address_space(1))) dv2 gd2;
-typedef __attribute__((address_space(1))) double gdbl;
-__device__ __forceinline__ gd2* gptr(double2* p) { return (gd2*)p; }
-__device__ __forceinline__ const gdbl* gptr(const double* p) { return (const gdbl*)p; }
-__device__ __forceinline__ double2 gld(const gd2* p, size_t i) {
-  const dv2 v = p[i];
-  return make_double2(v.x, v.y);
-}
-__device__ __forceinline__ void gst(gd2* p, size_t i, double2 a) {
-  dv2 v;
-  v.x = a.x;
-  v.y = a.y;
-  p[i] = v;
-}
-
-// Cooperative copy of n16 16-byte granules from global memory into LDS.
-__device__ __forceinline__ void stage16(void* dst, const void* src, int n16, int tid, int nt) {
-  const gd2* s = (const gd2*)src;
-  dv2* d = (dv2*)dst;
-  for (int i = tid; i < n16; i += nt) d[i] = s[i];
-}
-
-// Recurrence + propagator accumulation for one amplitude (see CoefK):
-//   MODE_APPLY  wdst = H w
-//   MODE_FIRST  w1 = s1 * (H - beta) w0,  acc = c1 w0 + c2 w1
-//   MODE_GEN    w_k = s2 * (H - beta) w_{k-1} - w_{k-2} (in place),  acc += c0 w_{k-2} + c1 w_{k-1} + c2 w_k
-__device__ __forceinline__ double2 gld(const double2* p, size_t i) { return p[i]; }
-__device__ __forceinline__ void gst(double2* p, size_t i, double2 a) { p[i] = a; }
-
-template <int MODE, typename Ptr>
-__device__ __forceinline__ void step_epilogue(size_t x, double2 out, double2 own, double scale,
-                                              Ptr __restrict__ wdst, Ptr __restrict__ acc_b,
-                                              const CoefK& C, int no_reads) {
-  if (MODE == MODE_APPLY) {
-    gst(wdst, x, out);
-  } else if (MODE == MODE_FIRST) {
-    double2 w;
-    w.x = scale * out.x;
-    w.y = scale * out.y;
-    gst(wdst, x, w);
-    double2 a = make_double2(0.0, 0.0);
-    a = cmad(a, C.c[1].x, C.c[1].y, own);
-    a = cmad(a, C.c[2].x, C.c[2].y, w);
-    gst(acc_b, x, a);
-  } else {
-    const double2 prev = no_reads ? make_double2(0.0, 0.0) : gld(wdst, x);
-    double2 w;
-    w.x = fma(scale, out.x, -prev.x);
-    w.y = fma(scale, out.y, -prev.y);
-    gst(wdst, x, w);
-    if (C.upd) {
-      double2 a = no_reads ? make_double2(0.0, 0.0) : gld(acc_b, x);
-      a = cmad(a, C.c[0].x, C.c[0].y, prev);
-      a = cmad(a, C.c[1].x, C.c[1].y, own);
-      a = cmad(a, C.c[2].x, C.c[2].y, w);
-      gst(acc_b, x, a);
-    }
-  }
-}
-
-// Per-tile diagonal pieces: s_c[i] = F_i(h) for tile bits i < L, s_c[L] = C(h).
-//   D(x) = zzlo[x_lo] + C(h) + sum_{i<L} F_i(h) s_i(x_lo)
-//   F_i(h) = field_i + sum_{j>=L} zz_ij s_j(h)
-//   C(h)   = shift - beta + sum_{j>=L} field_j s_j(h) + sum_{L<=i<j} zz_ij s_i(h) s_j(h)
-template <int L>
-__device__ __forceinline__ void tile_diag_coeffs(const DevProb& P, uint32_t h, double beta,
-                                                 double* s_c, int tid) {
-  const int n = P.n;
-  if (tid < L) {
-    double f = P.field[tid];
-    for (int j = L; j < n; ++j) f += P.zz[tid * n + j] * (0.5 - (double)((h >> (j - L)) & 1u));
-    s_c[tid] = f;
-  } else if (tid == L) {
-    double c = P.shift - beta;
-    for (int j = L; j < n; ++j) {
-      const double sj = 0.5 - (double)((h >> (j - L)) & 1u);
-      c += P.field[j] * sj;
-      for (int i = L; i < j; ++i) c += P.zz[i * n + j] * ((0.5 - (double)((h >> (i - L)) & 1u)) * sj);
-    }
-    s_c[L] = c;
-  }
-}
 
 template <int L, int MODE>
 __global__ void __launch_bounds__(Geo<L>::NT)
@@ -366,34 +263,11 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
 // ------------------------------------------------------------------------------------------
 // register-block step kernel
 // ------------------------------------------------------------------------------------------
-template <int L>
-struct RB {
-  static constexpr int T = 1 << L;
-  static constexpr int NT = T >> kRegBits;  // threads per workgroup
-  static constexpr int TB = L - kRegBits;    // tile bits carried by the thread index
-};
-
-// Upper bounds of the cross-tile term lists for a 34-qubit register (static LDS staging).
-template <int L>
-struct HiCap {
-  static constexpr int HB = DSE_MAX_HIGH_BITS(L);
-  static constexpr int PAIRS = HB * L + HB * (HB - 1) / 2 + 1;
-  static constexpr int FLIPS = HB + 1;
-};
-
 template <int L, int MODE>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int k, int q, int set) {
-  constexpr int NT = RB<L>::NT, TB = RB<L>::TB;
-  constexpr int NTT = TB * (TB - 1) / 2;
-  __shared__ double2 s_w[RB<L>::T];
-  __shared__ double s_c[L + 1];
-  // per-problem term tables, staged once per workgroup (vector loads of generic pointers inside
-  // the loops would serialise every iteration behind a global-memory round trip)
-  __shared__ DSweep s_sw[TB];
-  __shared__ DPair s_tt[NTT > 0 ? NTT : 1];
-  __shared__ DPair s_ph[HiCap<L>::PAIRS];
-  __shared__ DFlip s_fh[HiCap<L>::FLIPS];
+  constexpr int NT = RB<L>::NT;
+  __shared__ RBShared<L> S;
 
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
@@ -402,7 +276,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   if (MODE == MODE_GEN && k > P.degree) return;  // uniform: this problem's interval is done
 
   const int ab = g_dse_ablate;
-  const int n_tt = P.n_pairs_tt, n_ph = P.n_pairs_hi, n_fh = P.n_flips_hi;
+  const int n_ph = P.n_pairs_hi, n_fh = P.n_flips_hi;
   gd2* psi_b = gptr(P.buf[q ? 2 : 0]);
   gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
   gd2* scr_b = gptr(P.buf[1]);
@@ -420,112 +294,37 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   }
   const size_t base = (size_t)h << L;
 
-  stage16(s_sw, P.sweeps, TB * (int)(sizeof(DSweep) / 16), tid, NT);
-  stage16(s_tt, P.pairs_tt, n_tt, tid, NT);
-  stage16(s_ph, P.pairs_hi, n_ph, tid, NT);
-  stage16(s_fh, P.flips_hi, n_fh * (int)(sizeof(DFlip) / 16), tid, NT);
+  rb_stage_tables<L>(S, P, h, MODE == MODE_APPLY ? 0.0 : P.beta, tid);
 #pragma unroll
   for (int r = 0; r < 8; ++r)
-    s_w[r * NT + tid] = (ab & 32) ? make_double2(1.0, 0.0) : gld(win, base + r * NT + tid);
-  tile_diag_coeffs<L>(P, h, MODE == MODE_APPLY ? 0.0 : P.beta, s_c, tid);
-  const gdbl* zzlo = gptr(P.zzlo);
-  double zd[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) zd[r] = (ab & 16) ? 0.0 : zzlo[r * NT + tid];
+    S.w[r * NT + tid] = (ab & 32) ? make_double2(1.0, 0.0) : gld(win, base + r * NT + tid);
+  __syncthreads();
+  rb_register_zz<L>(S, tid);
+  const ThreadDiag td = rb_thread_diag<L>(S, tid);
   __syncthreads();
 
   // The first cross-tile flip (the rare drive in the center geometry) reads the partner tile
-  // elementwise: issue those loads now so their latency hides under the LDS work below.
+  // elementwise: issue those loads now so their latency hides under the sweeps.
   const bool pre = (n_fh > 0) && !(ab & 4);
   double2 part[8];
   if (pre) {
-    const DFlip F = s_fh[0];
+    const DFlip F = S.fh[0];
     const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
 #pragma unroll
     for (int r = 0; r < 8; ++r) part[r] = gld(src, (uint32_t)(r * NT + tid) ^ F.mask_lo);
   }
 
-  // ---- diagonal + register-bit terms (own amplitudes) ----
   double2 out[8];
-  {
-    double2 own[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) own[r] = s_w[r * NT + tid];
-    double gt = s_c[L];
-#pragma unroll
-    for (int i = 0; i < TB; ++i) gt += s_c[i] * (0.5 - (double)((tid >> i) & 1));
-    const double fa = 0.5 * s_c[TB], fb = 0.5 * s_c[TB + 1], fc = 0.5 * s_c[TB + 2];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const double d = zd[r] + gt + ((r & 1) ? -fa : fa) + ((r & 2) ? -fb : fb) + ((r & 4) ? -fc : fc);
-      out[r].x = d * own[r].x;
-      out[r].y = d * own[r].y;
-    }
-    if (P.rflip_mask) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        if (!((P.rflip_mask >> i) & 1)) continue;
-        const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const bool v = (r >> i) & 1;
-          out[r] = cmad(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
-        }
-      }
-    }
-#pragma unroll
-    for (int pp = 0; pp < 3; ++pp) {
-      const int a = (pp == 2) ? 1 : 0, b = (pp == 0) ? 1 : 2;
-      const double g = P.rr_g[pp];
-      if (g == 0.0) continue;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
-        const double2 sv = own[r ^ ((1 << a) | (1 << b))];
-        out[r].x = fma(g, sv.x, out[r].x);
-        out[r].y = fma(g, sv.y, out[r].y);
-      }
-    }
-  }
+  rb_apply_tile_a<L>(S, P, tid, td, ab, out);
 
-  // ---- thread bits: one LDS sweep of the partner thread per bit j ----
-  for (int j = 0; j < ((ab & 1) ? 0 : TB); ++j) {
-    const DSweep S = s_sw[j];
-    if (!(S.has_flip | S.has_pair)) continue;
-    const int bj = (tid >> j) & 1;
-    const int pt = tid ^ (1 << j);
-    double2 pv[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) pv[r] = s_w[r * NT + pt];
-    if (S.has_flip) {
-      const double cr = bj ? S.re1 : S.re0, ci = bj ? S.im1 : S.im0;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) out[r] = cmad(out[r], cr, ci, pv[r]);
-    }
-    if (S.has_pair) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const double g = S.g[i];
-        const double g0 = bj ? 0.0 : g, g1 = bj ? g : 0.0;  // pair applies iff bit_i(r) == bj
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const double gg = ((r >> i) & 1) ? g1 : g0;
-          const double2 sv = pv[r ^ (1 << i)];
-          out[r].x = fma(gg, sv.x, out[r].x);
-          out[r].y = fma(gg, sv.y, out[r].y);
-        }
-      }
-    }
-  }
-  // ---- the prefetched first cross-tile flip (loads issued before the sweeps) ----
   if (pre) {
-    const DFlip F = s_fh[0];
+    const DFlip F = S.fh[0];
     const bool v = par32(h & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
 #pragma unroll
     for (int r = 0; r < 8; ++r) out[r] = cmad(out[r], cr, ci, part[r]);
   }
-  // ---- epilogue operand w_{k-2}: issued now, its latency hides under the pair loop ----
+  // epilogue operand w_{k-2}: issued now, its latency hides under the thread-pair loop
   CoefK C = {};
   if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
   const bool rd = (MODE == MODE_GEN) && !(ab & 8);
@@ -535,51 +334,39 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
     for (int r = 0; r < 8; ++r) prev[r] = gld(wdst, base + r * NT + tid);
   }
 
-  // ---- pairs between two thread bits ----
-  for (int p = 0; p < ((ab & 2) ? 0 : n_tt); ++p) {
-    const DPair Q = s_tt[p];
-    if (__popc((uint32_t)tid & Q.mask_lo) & 1) continue;
-    const int pt = tid ^ (int)Q.mask_lo;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const double2 sv = s_w[r * NT + pt];
-      out[r].x = fma(Q.g, sv.x, out[r].x);
-      out[r].y = fma(Q.g, sv.y, out[r].y);
-    }
-  }
+  rb_apply_tile_b<L>(S, P, tid, ab, out);
 
-  // ---- terms reaching other tiles (global, L2/MALL-served) ----
-  // (processed four registers at a time to bound register pressure)
+  // ---- remaining cross-tile terms (global, L2/MALL-served), four registers at a time ----
   for (int f = 1; f < ((ab & 4) ? 0 : n_fh); ++f) {
-    const DFlip F = s_fh[f];
+    const DFlip F = S.fh[f];
     const bool v = par32(h & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
     const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
 #pragma unroll
-    for (int hr = 0; hr < 8; hr += 4) {
+    for (int hr4 = 0; hr4 < 8; hr4 += 4) {
       double2 sv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr + r) * NT + tid) ^ F.mask_lo);
+      for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr4 + r) * NT + tid) ^ F.mask_lo);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[hr + r] = cmad(out[hr + r], cr, ci, sv[r]);
+      for (int r = 0; r < 4; ++r) out[hr4 + r] = cmad(out[hr4 + r], cr, ci, sv[r]);
     }
   }
   for (int p = 0; p < ((ab & 4) ? 0 : n_ph); ++p) {
-    const DPair Q = s_ph[p];
+    const DPair Q = S.ph[p];
     const int hpar = par32(h & Q.tile_xor);
     if (Q.mask_lo == 0u && hpar) continue;  // both bits above the tile: uniform condition
     const gd2* src = win + ((size_t)(h ^ Q.tile_xor) << L);
 #pragma unroll
-    for (int hr = 0; hr < 8; hr += 4) {
+    for (int hr4 = 0; hr4 < 8; hr4 += 4) {
       double2 sv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr + r) * NT + tid) ^ Q.mask_lo);
+      for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr4 + r) * NT + tid) ^ Q.mask_lo);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t x = (uint32_t)((hr + r) * NT + tid);
+        const uint32_t x = (uint32_t)((hr4 + r) * NT + tid);
         const double g = ((__popc(x & Q.mask_lo) + hpar) & 1) ? 0.0 : Q.g;
-        out[hr + r].x = fma(g, sv[r].x, out[hr + r].x);
-        out[hr + r].y = fma(g, sv[r].y, out[hr + r].y);
+        out[hr4 + r].x = fma(g, sv[r].x, out[hr4 + r].x);
+        out[hr4 + r].y = fma(g, sv[r].y, out[hr4 + r].y);
       }
     }
   }
@@ -595,7 +382,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const size_t x = base + r * NT + tid;
-    const double2 own = s_w[r * NT + tid];
+    const double2 own = S.w[r * NT + tid];
     if (MODE == MODE_APPLY) {
       gst(wdst, x, out[r]);
     } else if (MODE == MODE_FIRST) {

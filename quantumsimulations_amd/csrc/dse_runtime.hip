@@ -47,16 +47,19 @@ struct HostProblem {
   CoefK* coef = nullptr;
   size_t coef_bytes = 0;
   int degree = 1;
+  double flops_per_amp = 0.0;  // algorithmic flops of one H application per amplitude
   int2* d_items = nullptr;  // this problem's tiles (apply_h / observables hooks)
 };
 
 // One stream's share of the problems, grouped by tile size.
 struct LaneGroup {
   int L = 0;
+  int tiles = 1;            // tiles per problem (persistent mode: 1 or 2)
   int64_t off = 0;          // first position in the global item array
   int64_t count = 0;        // items of this group
   std::vector<int> active;     // active[k] = items with degree >= k (prefix of the group)
   std::vector<double> bytes;   // bytes[k] = algorithmic HBM bytes of the term-k launch
+  std::vector<double> flops;   // flops[k] = algorithmic flops of the term-k launch
 };
 struct Lane {
   hipStream_t stream = nullptr;
@@ -86,6 +89,10 @@ struct dse_ctx {
   int last_q = 0;
   int tile_bits = 13;
   int n_streams = 4;
+  int persistent = 1;               // use k_interval when every problem fits <= 2 tiles
+  int n_cu = 256;                   // resident workgroups per launch of the 2-tile kernel
+  int* d_flags = nullptr;           // hand-off flags (2 per problem) + error word
+  size_t flags_cap = 0;
   int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
   double max_degree = 2e6;
@@ -122,6 +129,8 @@ void free_device(dse_ctx* ctx) {
   if (ctx->d_items) (void)hipFree(ctx->d_items), ctx->d_items = nullptr;
   if (ctx->d_partial) (void)hipFree(ctx->d_partial), ctx->d_partial = nullptr;
   for (auto& kv : ctx->zzlo_tables) (void)hipFree(kv.second);
+  if (ctx->d_flags) (void)hipFree(ctx->d_flags), ctx->d_flags = nullptr;
+  ctx->flags_cap = 0;
   ctx->zzlo_tables.clear();
   ctx->partial_slots = 0;
   ctx->total_items = 0;
@@ -417,6 +426,11 @@ dse_ctx* dse_create(int device) {
     return nullptr;
   }
   ctx->device = device;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+      ctx->n_cu = ncu;
+  }
   if (ensure_lanes(ctx) != DSE_OK) {
     g_create_err = "stream creation failed: " + ctx->err;
     delete ctx;
@@ -453,11 +467,14 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     ctx->n_streams = (int)value;
     ctx->evolved = false;
     return ensure_lanes(ctx);
+  } else if (k == "persistent") {
+    ctx->persistent = value != 0.0;
   } else if (k == "time_kernels") {
     if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
     ctx->time_every = (int)value;
   } else if (k == "ablate") {  // diagnostics only: skip kernel sections (results become wrong)
     HIPC(set_ablate((int)value));
+    HIPC(set_ablate_interval((int)value));
   } else if (k == "probe_items") {  // diagnostics only: dse_time_step_kernel launches this many items
     ctx->probe_items = (int64_t)value;
   } else if (k == "max_degree") {
@@ -506,6 +523,15 @@ int dse_add_problem(dse_ctx* ctx, int n, const double* field, const double* zz, 
   p.rare_bit = rare_bit;
   p.rare_z = rare_z_const;
   dse_spectral_bounds(n, p.field.data(), p.zz.data(), p.pair.data(), p.flip.data(), shift, &p.e_min, &p.e_max);
+  {  // diagonal 4, drive flip 8 (complex coefficient), pair 4 on the half of the rows where it acts
+    double f = 4.0;
+    for (int b = 0; b < n; ++b)
+      if (p.flip[4 * b] != 0.0 || p.flip[4 * b + 1] != 0.0) f += 8.0;
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j)
+        if (p.pair[i * n + j] != 0.0) f += 2.0;
+    p.flops_per_amp = f;
+  }
   (void)hipSetDevice(ctx->device);
   (void)sync_all(ctx);
   free_device(ctx);  // device layout is rebuilt lazily
@@ -663,15 +689,28 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   }
   HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
 
-  // ---- lanes: problems by degree (desc) dealt round-robin over the streams, grouped by tile ----
+  // ---- execution mode and lanes ----
+  // persistent: every problem fits one or two register-block tiles -> one k_interval launch per
+  // interval and lane; 2-tile problems on lane 0 (their workgroup pairs must be co-resident),
+  // 1-tile problems on lane 1.  streaming: problems by degree dealt round-robin over the lanes.
+  bool persistent = ctx->persistent != 0;
+  for (auto& P : ctx->probs)
+    if (!(interval_supported(P.L) && P.n_tiles <= 2)) persistent = false;
   const int n_lanes = std::min<int>(ctx->n_streams, (int)ctx->probs.size());
   std::vector<int> order(ctx->probs.size());
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
     return ctx->probs[a].degree > ctx->probs[b].degree;
   });
-  std::vector<std::map<int, std::vector<int>>> lane_probs(n_lanes);  // lane -> L -> problems
-  for (size_t i = 0; i < order.size(); ++i) lane_probs[i % n_lanes][ctx->probs[order[i]].L].push_back(order[i]);
+  // lane -> (L, tiles per problem) -> problems
+  std::vector<std::map<std::pair<int, int64_t>, std::vector<int>>> lane_probs(n_lanes);
+  for (size_t i = 0; i < order.size(); ++i) {
+    const HostProblem& P = ctx->probs[order[i]];
+    const std::pair<int, int64_t> key(P.L, P.n_tiles);
+    int lane = (int)(i % n_lanes);
+    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1) ? 0 : 1;
+    lane_probs[lane][key].push_back(order[i]);
+  }
   std::vector<int2> items;
   items.reserve(ctx->total_items);
   ctx->item_pos.assign(ctx->probs.size(), 0);
@@ -683,7 +722,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     if (li >= n_lanes) continue;
     for (auto& kv : lane_probs[li]) {
       LaneGroup g;
-      g.L = kv.first;
+      g.L = kv.first.first;
+      g.tiles = (int)kv.first.second;
       g.off = (int64_t)items.size();
       for (int pi : kv.second) {  // already in degree order
         ctx->item_pos[pi] = (int64_t)items.size();
@@ -694,26 +734,40 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       const int gdeg = ctx->probs[kv.second.front()].degree;
       g.active.assign(gdeg + 2, 0);
       g.bytes.assign(gdeg + 2, 0.0);
+      g.flops.assign(gdeg + 2, 0.0);
       const double T = (double)(int64_t(1) << g.L);
       for (int k = 0; k <= gdeg + 1; ++k) {
         int64_t c = 0;
-        double by = 0.0;
+        double by = 0.0, fl = 0.0;
         for (int pi : kv.second) {
           const int K = ctx->probs[pi].degree;
           if (K < k) continue;
           c += ctx->probs[pi].n_tiles;
+          fl += (double)ctx->probs[pi].n_tiles * T * ctx->probs[pi].flops_per_amp;
           // read w_{k-1}, read+write w_{k-2}/w_k (48 B/amp), plus acc read+write on update terms
           const bool upd = (k >= 2) && (((k - 1) % 3 == 0) || k == K);
           by += (double)ctx->probs[pi].n_tiles * T * (upd ? 80.0 : 48.0);
         }
         g.active[k] = (int)c;
         g.bytes[k] = by;
+        g.flops[k] = fl;
       }
       ln.groups.push_back(std::move(g));
     }
     max_deg = std::max(max_deg, ln.max_deg);
   }
   HIPC(hipMemcpy(ctx->d_items, items.data(), items.size() * sizeof(int2), hipMemcpyHostToDevice));
+  if (persistent) {
+    const size_t need = 2 * ctx->probs.size() + 1;
+    if (ctx->flags_cap < need) {
+      if (ctx->d_flags) (void)hipFree(ctx->d_flags), ctx->d_flags = nullptr;
+      if (hipMalloc(&ctx->d_flags, need * sizeof(int)) != hipSuccess)
+        return fail(ctx, DSE_ERR_OOM, "flag allocation failed");
+      ctx->flags_cap = need;
+    }
+    HIPC(hipMemset(ctx->d_flags, 0, need * sizeof(int)));
+  }
+  int* d_err = persistent ? ctx->d_flags + 2 * ctx->probs.size() : nullptr;
 
   // ---- psi(t0) = |psi0> ----
   hipStream_t st0 = ctx->lanes[0].stream;
@@ -733,8 +787,9 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       if ((rc = ensure_events(ctx, ln, (size_t)ln.groups.size() * (ln.max_deg + 1) + 1))) return rc;
 
   double step_ms = 0.0, launches_timed = 0.0, bytes_timed = 0.0;
-  double launches = 0.0, amp_updates = 0.0, all_bytes = 0.0;
-  std::vector<std::vector<double>> pool_bytes(ctx->lanes.size() * 2);
+  double launches = 0.0, amp_updates = 0.0, all_bytes = 0.0, all_flops = 0.0, flops_timed = 0.0;
+  // per timed launch: algorithmic flops (pool_bytes) and HBM bytes (pool_bytes2, streaming only)
+  std::vector<std::vector<double>> pool_bytes(ctx->lanes.size() * 2), pool_bytes2(ctx->lanes.size() * 2);
   auto drain = [&](Lane& ln, size_t li, int pool) -> int {
     if (ln.ev_used[pool] == 0) return DSE_OK;
     HIPC(hipEventSynchronize(ln.ev[pool][2 * ln.ev_used[pool] - 1]));
@@ -742,11 +797,13 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       float ms = 0.f;
       HIPC(hipEventElapsedTime(&ms, ln.ev[pool][2 * i], ln.ev[pool][2 * i + 1]));
       step_ms += ms;
-      bytes_timed += pool_bytes[li * 2 + pool][i];
+      flops_timed += pool_bytes[li * 2 + pool][i];
+      if (i < pool_bytes2[li * 2 + pool].size()) bytes_timed += pool_bytes2[li * 2 + pool][i];
     }
     launches_timed += (double)ln.ev_used[pool];
     ln.ev_used[pool] = 0;
     pool_bytes[li * 2 + pool].clear();
+    pool_bytes2[li * 2 + pool].clear();
     return DSE_OK;
   };
   auto obs_all = [&](int bsel_q, size_t slot) -> int {
@@ -772,6 +829,33 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       if ((rc = drain(ln, li, pool))) return rc;
       for (auto& g : ln.groups) {
         const int T = 1 << g.L;
+        if (persistent) {
+          // all K terms of the interval in one launch; 2-tile groups in co-resident chunks
+          if (g.tiles == 2) HIPC(hipMemsetAsync(ctx->d_flags, 0, 2 * ctx->probs.size() * sizeof(int), ln.stream));
+          const int64_t cap = g.tiles == 2 ? std::max<int64_t>(2, (ctx->n_cu / 2) * 2) : g.count;
+          for (int64_t off = 0; off < g.count; off += cap) {
+            const int cnt = (int)std::min<int64_t>(cap, g.count - off);
+            double fl = 0.0, am = 0.0;
+            for (int64_t i = off; i < off + cnt; ++i) {
+              const HostProblem& P = ctx->probs[items[g.off + i].x];
+              am += (double)T * P.degree;
+              fl += (double)T * P.degree * P.flops_per_amp;
+            }
+            if (timed) {
+              const size_t i = ln.ev_used[pool]++;
+              HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
+              HIPC(launch_interval(g.L, ctx->d_probs, ctx->d_items + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
+              HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
+              pool_bytes[li * 2 + pool].push_back(fl);
+            } else {
+              HIPC(launch_interval(g.L, ctx->d_probs, ctx->d_items + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
+            }
+            launches += 1.0;
+            amp_updates += am;
+            all_flops += fl;
+          }
+          continue;
+        }
         HIPC(launch_step(g.L, MODE_FIRST, ctx->d_probs, ctx->d_items + g.off, g.active[1], 1, q, set, ln.stream));
         for (int k = 2; k < (int)g.active.size(); ++k) {
           const int na = g.active[k];
@@ -781,13 +865,15 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
             HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
             HIPC(launch_step(g.L, MODE_GEN, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
             HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
-            pool_bytes[li * 2 + pool].push_back(g.bytes[k]);
+            pool_bytes[li * 2 + pool].push_back(g.flops[k]);
+            pool_bytes2[li * 2 + pool].push_back(g.bytes[k]);
           } else {
             HIPC(launch_step(g.L, MODE_GEN, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
           }
           launches += 1.0;
           amp_updates += (double)na * T;
           all_bytes += g.bytes[k];
+          all_flops += g.flops[k];
         }
       }
     }
@@ -807,6 +893,11 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     for (int pool = 0; pool < 2; ++pool)
       if ((rc = drain(ctx->lanes[li], li, pool))) return rc;
   if ((rc = sync_all(ctx))) return rc;
+  if (persistent) {
+    int herr = 0;
+    HIPC(hipMemcpy(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr) return fail(ctx, DSE_ERR_HIP, "cross-tile hand-off timed out (workgroup pair not co-resident)");
+  }
   ctx->last_q = (n_t - 1) & 1;
   ctx->evolved = true;
 
@@ -817,6 +908,9 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->h_applications = happl;
     stats->amplitude_updates = amp_updates;
     stats->step_bytes = all_bytes;
+    stats->h_flops = all_flops;
+    stats->timed_flops = flops_timed;
+    stats->mode = persistent ? 1 : 0;
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
     stats->step_launches = launches;
     stats->timed_launches = launches_timed;

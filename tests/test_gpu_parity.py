@@ -232,3 +232,33 @@ def test_simulate_rare_drop_in_contract():
         assert v.dtype == np.float64 and v.shape == (201,)
     with pytest.raises(ValueError):
         simulate_rare(dataclasses.replace(p, steps=1))
+
+
+@pytest.mark.parametrize("n,tile_bits", [(10, 9), (12, 12), (13, 12), (14, 13)])
+def test_persistent_matches_streaming_and_expm(engine, n, tile_bits):
+    """The persistent interval kernel (1- and 2-tile registers, cross-tile hand-off) reproduces
+    the per-term streaming kernels and scipy's expm_multiply."""
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import expm_multiply
+    from quantumsimulations_amd.dipolar_ensemble_with_rare import problem_to_csr
+    probs = [_random_problem(n, 300 + n + s, rare_bit=n - 1) for s in range(3)]
+    t = np.linspace(0.0, 5e-4, 4)
+    res, states = {}, {}
+    engine.set_option("tile_bits", tile_bits)
+    try:
+        for pers in (0, 1):
+            engine.clear()
+            engine.set_option("persistent", pers)
+            for p in probs:
+                engine.add(p)
+            res[pers], st = engine.evolve(t)
+            assert st["mode"] == pers
+            states[pers] = [engine.state(i) for i in range(len(probs))]
+    finally:
+        engine.set_option("persistent", 1)
+        engine.set_option("tile_bits", 13)
+    np.testing.assert_allclose(res[1], res[0], rtol=0, atol=1e-11)
+    psi0 = np.zeros(1 << n, dtype=complex)
+    psi0[probs[1].psi0_index] = 1.0
+    ref = expm_multiply(-1j * t[-1] * sp.csr_matrix(problem_to_csr(probs[1])), psi0)
+    assert np.max(np.abs(states[1][1] - ref)) < 1e-10
