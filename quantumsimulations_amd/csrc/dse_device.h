@@ -43,6 +43,34 @@ __device__ __forceinline__ void gst(gd2* p, size_t i, double2 a) {
   p[i] = v;
 }
 
+// Buffer-resource views of one tile (wave-uniform base, 32-bit byte offsets): per-register
+// accesses become buffer ops with the register offset in an SGPR instead of one 64-bit VGPR
+// address per register.  aux = kSc1 makes a store write-through to the coherence point and a load
+// bypass the non-coherent L1 (cross-workgroup hand-off, MI355X_MICROARCH.md Valid forms row 1).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const double2* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)bytes,
+                                           0x00020000);
+}
+template <int AUX = 0>
+__device__ __forceinline__ double2 bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, AUX);
+  const dv2 d = __builtin_bit_cast(dv2, v);
+  return make_double2(d.x, d.y);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                    double2 a) {
+  dv2 d;
+  d.x = a.x;
+  d.y = a.y;
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d), r, (int)voff, (int)soff, AUX);
+}
+
 // Cooperative copy of n16 16-byte granules from global memory into LDS.
 __device__ __forceinline__ void stage16(void* dst, const void* src, int n16, int tid, int nt) {
   const gd2* s = (const gd2*)src;
@@ -114,6 +142,7 @@ __device__ __forceinline__ void tile_diag_coeffs(const DevProb& P, uint32_t h, d
 template <int L>
 struct RB {
   static constexpr int T = 1 << L;
+  static constexpr int R = kRegAmps;         // amplitudes per thread
   static constexpr int NT = T >> kRegBits;  // threads per workgroup
   static constexpr int TB = L - kRegBits;    // tile bits carried by the thread index
 };
@@ -130,8 +159,8 @@ struct HiCap {
 // ------------------------------------------------------------------------------------------
 // Register-block application of the in-tile part of H (LDS only)
 // ------------------------------------------------------------------------------------------
-// Workgroup-shared state of the register-block kernels.  One thread owns the 8 amplitudes
-// x = r * NT + tid (r = 0..7): the three top tile bits are register bits.
+// Workgroup-shared state of the register-block kernels.  One thread owns the R = 16 amplitudes
+// x = r * NT + tid (r = 0..15): the four top tile bits are register bits.
 template <int L>
 struct RBShared {
   static constexpr int TB = RB<L>::TB;
@@ -139,7 +168,7 @@ struct RBShared {
   double2 w[RB<L>::T];               // the tile of w_{k-1}
   double c[L + 1];                   // F_i(h) (i < L) and C(h) of the tile
   double zz[L * L];                  // in-tile zz couplings (row-major, upper triangle)
-  double zr[8];                      // register-bit ZZ part of the diagonal per r
+  double zr[kRegAmps];               // register-bit ZZ part of the diagonal per r
   DSweep sw[TB];                     // thread-bit sweeps
   DPair tt[NTT > 0 ? NTT : 1];       // thread-bit pairs
   DPair ph[HiCap<L>::PAIRS];         // cross-tile pairs
@@ -169,84 +198,108 @@ __device__ __forceinline__ void rb_stage_tables(RBShared<L>& S, const DevProb& P
 //   zt    = C(h) + sum_{j<TB} F_j s_j(tid) + sum_{i<j<TB} zz_ij s_i(tid) s_j(tid)
 //   hr[i] = F_{TB+i} + sum_{j<TB} zz_{j,TB+i} s_j(tid)
 struct ThreadDiag {
-  double zt, h0, h1, h2;
+  double zt;
+  double hr[kRegBits];
 };
 
 template <int L>
 __device__ __forceinline__ ThreadDiag rb_thread_diag(const RBShared<L>& S, int tid) {
   constexpr int TB = RB<L>::TB;
-  double z = S.c[L], h0 = S.c[TB], h1 = S.c[TB + 1], h2 = S.c[TB + 2];
+  ThreadDiag d;
+  d.zt = S.c[L];
+#pragma unroll
+  for (int i = 0; i < kRegBits; ++i) d.hr[i] = S.c[TB + i];
 #pragma unroll 1
   for (int j = 0; j < TB; ++j) {
     const double sj = 0.5 - (double)((tid >> j) & 1);
     double a = S.c[j];
 #pragma unroll 1
     for (int i = j + 1; i < TB; ++i) a += S.zz[j * L + i] * (0.5 - (double)((tid >> i) & 1));
-    z += a * sj;
-    h0 += S.zz[j * L + TB] * sj;
-    h1 += S.zz[j * L + TB + 1] * sj;
-    h2 += S.zz[j * L + TB + 2] * sj;
+    d.zt += a * sj;
+#pragma unroll
+    for (int i = 0; i < kRegBits; ++i) d.hr[i] += S.zz[j * L + TB + i] * sj;
   }
-  return ThreadDiag{z, h0, h1, h2};
+  return d;
 }
 
-// zr[r] for the 8 register patterns (one thread per entry; needs S.zz after a barrier)
+// zr[r] for the register patterns (one thread per entry; needs S.zz after a barrier)
 template <int L>
 __device__ __forceinline__ void rb_register_zz(RBShared<L>& S, int tid) {
   constexpr int TB = RB<L>::TB;
-  if (tid < 8) {
+  if (tid < kRegAmps) {
     double v = 0.0;
-    for (int a = 0; a < 3; ++a)
-      for (int b = a + 1; b < 3; ++b)
+    for (int a = 0; a < kRegBits; ++a)
+      for (int b = a + 1; b < kRegBits; ++b)
         v += S.zz[(TB + a) * L + TB + b] * ((0.5 - ((tid >> a) & 1)) * (0.5 - ((tid >> b) & 1)));
     S.zr[tid] = v;
   }
 }
 
+// Pairs (thread bit j, register bit i) of one sweep for a wave-uniform bit value BJ of thread
+// bit j: the pair applies iff bit_i(r) == BJ, so only those registers are touched.
+template <int BJ>
+__device__ __forceinline__ void rb_sweep_pairs_uniform(const DSweep& Sw, const double2* pv,
+                                                       double2* out) {
+#pragma unroll
+  for (int i = 0; i < kRegBits; ++i) {
+    const double g = Sw.g[i];
+#pragma unroll
+    for (int r = 0; r < kRegAmps; ++r) {
+      if (((r >> i) & 1) != BJ) continue;  // compile-time
+      const double2 sv = pv[r ^ (1 << i)];
+      out[r].x = fma(g, sv.x, out[r].x);
+      out[r].y = fma(g, sv.y, out[r].y);
+    }
+  }
+}
+
 // out = (H - beta) w on the tile's own terms, part A: diagonal, register-bit drives/pairs and
-// thread-bit sweeps (one LDS read of the partner thread per bit, serving its drive and its 3 pairs
-// with register bits).  Part B (rb_apply_tile_b): pairs between two thread bits.  Cross-tile
-// terms are added by the caller.
+// thread-bit sweeps (one LDS read of the partner thread per bit, serving its drive and its
+// pairs with the register bits).  Part B (rb_apply_tile_b): pairs between two thread bits.
+// Cross-tile terms are added by the caller.
 template <int L>
 __device__ __forceinline__ void rb_apply_tile_a(const RBShared<L>& S, const DevProb& P, int tid,
-                                                const ThreadDiag& td, int ab, double2 out[8]) {
-  constexpr int NT = RB<L>::NT, TB = RB<L>::TB;
+                                                const ThreadDiag& td, int ab,
+                                                double2 out[kRegAmps]) {
+  constexpr int NT = RB<L>::NT, TB = RB<L>::TB, R = kRegAmps;
   {
-    double2 own[8];
+    double2 own[R];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) own[r] = S.w[r * NT + tid];
+    for (int r = 0; r < R; ++r) own[r] = S.w[r * NT + tid];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const double d = td.zt + ((r & 1) ? -0.5 : 0.5) * td.h0 + ((r & 2) ? -0.5 : 0.5) * td.h1 +
-                       ((r & 4) ? -0.5 : 0.5) * td.h2 + S.zr[r];
+    for (int r = 0; r < R; ++r) {
+      double d = td.zt + S.zr[r];
+#pragma unroll
+      for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * td.hr[i];
       out[r].x = d * own[r].x;
       out[r].y = d * own[r].y;
     }
     if (P.rflip_mask) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+      for (int i = 0; i < kRegBits; ++i) {
         if (!((P.rflip_mask >> i) & 1)) continue;
         const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < R; ++r) {
           const bool v = (r >> i) & 1;
           out[r] = cmad(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
         }
       }
     }
 #pragma unroll
-    for (int pp = 0; pp < 3; ++pp) {
-      const int a = (pp == 2) ? 1 : 0, b = (pp == 0) ? 1 : 2;
-      const double g = P.rr_g[pp];
-      if (g == 0.0) continue;
+    for (int a = 0; a < kRegBits; ++a)
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
-        const double2 sv = own[r ^ ((1 << a) | (1 << b))];
-        out[r].x = fma(g, sv.x, out[r].x);
-        out[r].y = fma(g, sv.y, out[r].y);
+      for (int b = a + 1; b < kRegBits; ++b) {
+        const double g = P.rr_g[rr_index(a, b)];
+        if (g == 0.0) continue;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
+          const double2 sv = own[r ^ ((1 << a) | (1 << b))];
+          out[r].x = fma(g, sv.x, out[r].x);
+          out[r].y = fma(g, sv.y, out[r].y);
+        }
       }
-    }
   }
 #pragma unroll 1
   for (int j = 0; j < ((ab & 1) ? 0 : TB); ++j) {
@@ -254,25 +307,32 @@ __device__ __forceinline__ void rb_apply_tile_a(const RBShared<L>& S, const DevP
     if (!(Sw.has_flip | Sw.has_pair)) continue;
     const int bj = (tid >> j) & 1;
     const int pt = tid ^ (1 << j);
-    double2 pv[8];
+    double2 pv[R];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) pv[r] = S.w[r * NT + pt];
+    for (int r = 0; r < R; ++r) pv[r] = S.w[r * NT + pt];
     if (Sw.has_flip) {
       const double cr = bj ? Sw.re1 : Sw.re0, ci = bj ? Sw.im1 : Sw.im0;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) out[r] = cmad(out[r], cr, ci, pv[r]);
+      for (int r = 0; r < R; ++r) out[r] = cmad(out[r], cr, ci, pv[r]);
     }
     if (Sw.has_pair) {
+      if (j >= 6) {  // a wave-index bit: bj is uniform, touch only the registers it pairs
+        if (bj)
+          rb_sweep_pairs_uniform<1>(Sw, pv, out);
+        else
+          rb_sweep_pairs_uniform<0>(Sw, pv, out);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const double g = Sw.g[i];
-        const double g0 = bj ? 0.0 : g, g1 = bj ? g : 0.0;  // pair applies iff bit_i(r) == bj
+        for (int i = 0; i < kRegBits; ++i) {
+          const double g = Sw.g[i];
+          const double g0 = bj ? 0.0 : g, g1 = bj ? g : 0.0;  // pair applies iff bit_i(r) == bj
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const double gg = ((r >> i) & 1) ? g1 : g0;
-          const double2 sv = pv[r ^ (1 << i)];
-          out[r].x = fma(gg, sv.x, out[r].x);
-          out[r].y = fma(gg, sv.y, out[r].y);
+          for (int r = 0; r < R; ++r) {
+            const double gg = ((r >> i) & 1) ? g1 : g0;
+            const double2 sv = pv[r ^ (1 << i)];
+            out[r].x = fma(gg, sv.x, out[r].x);
+            out[r].y = fma(gg, sv.y, out[r].y);
+          }
         }
       }
     }
@@ -281,7 +341,7 @@ __device__ __forceinline__ void rb_apply_tile_a(const RBShared<L>& S, const DevP
 
 template <int L>
 __device__ __forceinline__ void rb_apply_tile_b(const RBShared<L>& S, const DevProb& P, int tid,
-                                                int ab, double2 out[8]) {
+                                                int ab, double2 out[kRegAmps]) {
   constexpr int NT = RB<L>::NT;
   const int n_tt = (ab & 2) ? 0 : P.n_pairs_tt;
 #pragma unroll 1
@@ -290,7 +350,7 @@ __device__ __forceinline__ void rb_apply_tile_b(const RBShared<L>& S, const DevP
     if (__popc((uint32_t)tid & Q.mask_lo) & 1) continue;
     const int pt = tid ^ (int)Q.mask_lo;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < kRegAmps; ++r) {
       const double2 sv = S.w[r * NT + pt];
       out[r].x = fma(Q.g, sv.x, out[r].x);
       out[r].y = fma(Q.g, sv.y, out[r].y);

@@ -11,8 +11,14 @@ enum { MODE_APPLY = 0, MODE_FIRST = 1, MODE_GEN = 2 };
 
 constexpr int kMinTile = 1;
 constexpr int kMaxTile = 13;
-constexpr int kRegBlockMinTile = 9;  // tiles >= 2^9 use the register-block kernel
-constexpr int kRegBits = 3;          // amplitudes per thread = 2^kRegBits in that kernel
+constexpr int kRegBits = 4;                       // amplitudes per thread = 2^kRegBits in that kernel
+constexpr int kRegAmps = 1 << kRegBits;
+constexpr int kRegPairs = kRegBits * (kRegBits - 1) / 2;
+constexpr int kRegBlockMinTile = 6 + kRegBits;    // tiles >= 2^10 (>= one wave) use it
+// index of the register-bit pair (a, b), a < b, in DevProb::rr_g: (0,1) (0,2) (0,3) (1,2) ...
+__host__ __device__ constexpr int rr_index(int a, int b) {
+  return a * (2 * kRegBits - a - 1) / 2 + (b - a - 1);
+}
 // bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index
 #define DSE_MAX_HIGH_BITS(L) ((34 - (L)) < 0 ? 0 : (34 - (L)))
 
@@ -31,13 +37,13 @@ struct alignas(16) DFlip {
   double pad;
 };
 
-// Register-block kernel: one thread owns the 8 amplitudes x = rho * NT + tid (rho = 0..7),
-// i.e. the three top tile bits are "register bits".  For every thread bit j a sweep reads the
-// partner thread's 8 amplitudes once from LDS and applies (a) the drive flip of bit j and
-// (b) the pair flips (j, register bit i) for i = 0..2.
+// Register-block kernel: one thread owns the 16 amplitudes x = rho * NT + tid (rho = 0..15),
+// i.e. the four top tile bits are "register bits".  For every thread bit j a sweep reads the
+// partner thread's 16 amplitudes once from LDS and applies (a) the drive flip of bit j and
+// (b) the pair flips (j, register bit i) for i = 0..3.
 struct alignas(16) DSweep {
   double re0, im0, re1, im1;  // drive flip on thread bit j (zero when absent)
-  double g[3];                // pair coefficient with register bit i
+  double g[kRegBits];         // pair coefficient with register bit i
   uint32_t has_flip;
   uint32_t has_pair;
 };
@@ -61,15 +67,15 @@ struct DevProb {
   const DPair* pairs_hi;  // at least one bit above the tile (both kernels)
   const DFlip* flips_lo;  // generic kernel
   const DFlip* flips_hi;  // both kernels
-  const DSweep* sweeps;   // register-block kernel: [L-3] thread-bit sweeps
+  const DSweep* sweeps;   // register-block kernel: [L-kRegBits] thread-bit sweeps
   const DPair* pairs_tt;  // register-block kernel: pairs between two thread bits
   const CoefK* coef;      // [n_sets][kcap1] Chebyshev coefficients per term
   uint64_t sea_mask;
   double shift;
   double beta;            // spectral centre
   double s1;              // 1/alpha
-  double rr_g[3];         // register-block kernel: pairs (0,1) (0,2) (1,2) among register bits
-  double rflip[3][4];     // register-block kernel: drive flips on register bits (re0 im0 re1 im1)
+  double rr_g[kRegPairs]; // register-block kernel: pairs among register bits (rr_index order)
+  double rflip[kRegBits][4];  // register-block kernel: drive flips on register bits (re0 im0 re1 im1)
   int n, L;
   int n_pairs_lo, n_pairs_hi, n_flips_lo, n_flips_hi, n_pairs_tt;
   int kcap1;

@@ -4,7 +4,7 @@
 // one or two LDS tiles (n <= L + 1; the N = 14 sweep: center_off has n = 13, center_on and
 // shell_off n = 14).  Each workgroup owns one tile for all K terms of the interval:
 //   LDS        w_{k-1} (the tile being multiplied; 128 KiB at L = 13)
-//   registers  w_{k-2} (8 amplitudes per thread) and the new w_k
+//   registers  w_{k-2} (16 amplitudes per thread) and the new w_k
 //   global     acc (accumulated every third term, L2-resident) and, for 2-tile problems, the
 //              cross-tile contribution u published to the partner workgroup each term.
 // This replaces K launches of k_step_rb (each reloading the tile from HBM and writing w_k back)
@@ -35,20 +35,13 @@ namespace {
 
 typedef __attribute__((address_space(1))) int gint;
 
-__device__ __forceinline__ void st_sc1(gdbl* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const gdbl* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 constexpr int kSpinLimit = 1 << 22;  // ~0.3 s of polling before the hand-off is declared failed
 
 template <int L>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
            int* __restrict__ flags, int* __restrict__ err) {
-  constexpr int NT = RB<L>::NT;
+  constexpr int NT = RB<L>::NT, R = kRegAmps;
   constexpr size_t T = size_t(1) << L;
   __shared__ RBShared<L> S;
   __shared__ int s_fail;
@@ -61,15 +54,17 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const int K = P.degree;
   const double s1 = P.s1;
 
-  gd2* psi_b = gptr(P.buf[q ? 2 : 0]);
-  gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
-  // exchange slots: term parity 0 -> psi region (free once w_0 is in LDS), 1 -> scratch
-  gdbl* slot_me[2] = {(gdbl*)(psi_b + (h << L)), (gdbl*)(gptr(P.buf[1]) + (h << L))};
-  const gdbl* slot_pa[2] = {(const gdbl*)(psi_b + ((h ^ 1u) << L)),
-                            (const gdbl*)(gptr(P.buf[1]) + ((h ^ 1u) << L))};
+  // exchange slots (AoS double2, sc1): term parity 0 -> psi region (free once w_0 is in LDS),
+  // 1 -> scratch buffer
+  constexpr uint32_t TBYTES = uint32_t(T) * 16u;
+  const __amdgpu_buffer_rsrc_t slot_me[2] = {tile_rsrc(P.buf[q ? 2 : 0] + (h << L), TBYTES),
+                                             tile_rsrc(P.buf[1] + (h << L), TBYTES)};
+  const __amdgpu_buffer_rsrc_t slot_pa[2] = {tile_rsrc(P.buf[q ? 2 : 0] + ((h ^ 1u) << L), TBYTES),
+                                             tile_rsrc(P.buf[1] + ((h ^ 1u) << L), TBYTES)};
+  const __amdgpu_buffer_rsrc_t acc_t = tile_rsrc(P.buf[q ? 0 : 2] + (h << L), TBYTES);
+  const uint32_t voff = (uint32_t)tid * 16u;
   gint* flag_me = (gint*)flags + 2 * it.x + h;
   const gint* flag_pa = (const gint*)flags + 2 * it.x + (h ^ 1u);
-  const size_t base = (size_t)h << L;
   const uint32_t b_pa = (h ^ 1u) & 1u;  // top-bit value of the partner tile
 
   // diagnostics only (0 in production): 64 skip the u publication, 128 skip the partner wait and
@@ -78,35 +73,34 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   if (tid == 0) s_fail = 0;
   rb_stage_tables<L>(S, P, h, P.beta, tid);
 #pragma unroll
-  for (int r = 0; r < 8; ++r) S.w[r * NT + tid] = gld(psi_b, base + r * NT + tid);
+  for (int r = 0; r < R; ++r) S.w[r * NT + tid] = bld(slot_me[0], voff, (uint32_t)(r * NT * 16));
   __syncthreads();
   rb_register_zz<L>(S, tid);
   const ThreadDiag td = rb_thread_diag<L>(S, tid);
   __syncthreads();
 
-  double2 prev[8];
+  double2 prev[R];
   for (int k = 1; k <= K; ++k) {
-    // ---- u(w_{k-1}) for the partner: computed and stored (SoA, so every 8-byte sc1 store
-    // instruction writes 512 contiguous bytes) before the tile terms, published after them so
-    // the write-through drains under the compute ----
-    gdbl* dst = slot_me[(k - 1) & 1];
+    // ---- u(w_{k-1}) for the partner: computed and stored (16-byte sc1 stores) before the
+    // tile terms, published after them so the write-through drains under the compute ----
+    const __amdgpu_buffer_rsrc_t dst = slot_me[(k - 1) & 1];
     if (pair && !(ab & 64)) {
-      double2 u[8];
+      double2 u[R];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) u[r] = make_double2(0.0, 0.0);
+      for (int r = 0; r < R; ++r) u[r] = make_double2(0.0, 0.0);
       // cross flip of the top bit: coefficient for the partner's output bit value
       for (int f = 0; f < P.n_flips_hi; ++f) {
         const DFlip F = S.fh[f];
         const double cr = b_pa ? F.re1 : F.re0, ci = b_pa ? F.im1 : F.im0;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) u[r] = cmad(u[r], cr, ci, S.w[r * NT + tid]);
+        for (int r = 0; r < R; ++r) u[r] = cmad(u[r], cr, ci, S.w[r * NT + tid]);
       }
       // cross pairs (j, top): applies iff x_j == b_pa; source w_A(x ^ e_j)
       for (int p = 0; p < P.n_pairs_hi; ++p) {
         const DPair Q = S.ph[p];
         const uint32_t m = Q.mask_lo;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < R; ++r) {
           const uint32_t x = (uint32_t)(r * NT + tid);
           const double g = (((x & m) != 0u) == (b_pa != 0u)) ? Q.g : 0.0;
           const double2 sv = S.w[x ^ m];
@@ -115,17 +109,14 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         }
       }
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        st_sc1(dst + (r * NT + tid), u[r].x);
-        st_sc1(dst + T + (r * NT + tid), u[r].y);
-      }
+      for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), u[r]);
     }
 
     // ---- out = (H - beta) w_{k-1}: own-tile terms ----
-    double2 out[8];
+    double2 out[R];
     if (ab & 512) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) out[r] = S.w[r * NT + tid];
+      for (int r = 0; r < R; ++r) out[r] = S.w[r * NT + tid];
     } else {
       rb_apply_tile_a<L>(S, P, tid, td, 0, out);
       rb_apply_tile_b<L>(S, P, tid, 0, out);
@@ -150,56 +141,55 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         }
       }
       __syncthreads();
-      const gdbl* src = slot_pa[(k - 1) & 1];
-      double ur[8], ui[8];
+      const __amdgpu_buffer_rsrc_t src = slot_pa[(k - 1) & 1];
+      double2 uv[R];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        ur[r] = ld_sc1(src + (r * NT + tid));
-        ui[r] = ld_sc1(src + T + (r * NT + tid));
-      }
+      for (int r = 0; r < R; ++r) uv[r] = bld<kSc1>(src, voff, (uint32_t)(r * NT * 16));
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        out[r].x += ur[r];
-        out[r].y += ui[r];
+      for (int r = 0; r < R; ++r) {
+        out[r].x += uv[r].x;
+        out[r].y += uv[r].y;
       }
     }
 
-    // ---- recurrence + accumulation ----
+    // ---- recurrence + accumulation (in place in out[], acc operands four registers at a time
+    // to bound the live registers) ----
     const CoefK C = P.coef[set * P.kcap1 + k];
-    double2 accv[8];
     const bool upd = C.upd && !(ab & 256);
-    if (k > 1 && upd) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) accv[r] = gld(acc_b, base + r * NT + tid);
-    }
-    double2 w[8];
+    for (int r0 = 0; r0 < R; r0 += 4) {
+      double2 accv[4];
+      if (k > 1 && upd) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const size_t x = base + r * NT + tid;
-      const double2 own = S.w[r * NT + tid];
-      if (k == 1) {
-        w[r].x = s1 * out[r].x;
-        w[r].y = s1 * out[r].y;
-        double2 a = make_double2(0.0, 0.0);
-        a = cmad(a, C.c[1].x, C.c[1].y, own);
-        a = cmad(a, C.c[2].x, C.c[2].y, w[r]);
-        gst(acc_b, x, a);
-      } else {
-        w[r].x = fma(2.0 * s1, out[r].x, -prev[r].x);
-        w[r].y = fma(2.0 * s1, out[r].y, -prev[r].y);
-        if (upd) {
-          double2 a = accv[r];
-          a = cmad(a, C.c[0].x, C.c[0].y, prev[r]);
-          a = cmad(a, C.c[1].x, C.c[1].y, own);
-          a = cmad(a, C.c[2].x, C.c[2].y, w[r]);
-          gst(acc_b, x, a);
-        }
+        for (int r = 0; r < 4; ++r) accv[r] = bld(acc_t, voff, (uint32_t)((r0 + r) * NT * 16));
       }
-      prev[r] = own;
+#pragma unroll
+      for (int r = r0; r < r0 + 4; ++r) {
+        const double2 own = S.w[r * NT + tid];
+        if (k == 1) {
+          out[r].x *= s1;
+          out[r].y *= s1;
+          double2 a = make_double2(0.0, 0.0);
+          a = cmad(a, C.c[1].x, C.c[1].y, own);
+          a = cmad(a, C.c[2].x, C.c[2].y, out[r]);
+          bst(acc_t, voff, (uint32_t)(r * NT * 16), a);
+        } else {
+          out[r].x = fma(2.0 * s1, out[r].x, -prev[r].x);
+          out[r].y = fma(2.0 * s1, out[r].y, -prev[r].y);
+          if (upd) {
+            double2 a = accv[r - r0];
+            a = cmad(a, C.c[0].x, C.c[0].y, prev[r]);
+            a = cmad(a, C.c[1].x, C.c[1].y, own);
+            a = cmad(a, C.c[2].x, C.c[2].y, out[r]);
+            bst(acc_t, voff, (uint32_t)(r * NT * 16), a);
+          }
+        }
+        prev[r] = own;
+      }
     }
     __syncthreads();  // every read of w_{k-1} in LDS is done
 #pragma unroll
-    for (int r = 0; r < 8; ++r) S.w[r * NT + tid] = w[r];
+    for (int r = 0; r < R; ++r) S.w[r * NT + tid] = out[r];
     __syncthreads();
     if (s_fail) break;  // uniform: a hand-off timed out (error reported to the host)
   }
@@ -218,7 +208,7 @@ hipError_t launch_interval(int L, const DevProb* probs, const int2* items, int n
     hipLaunchKernelGGL((k_interval<l>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs, items, q, \
                        set, flags, err);                                                      \
     return hipGetLastError();
-    X(9) X(10) X(11) X(12) X(13)
+    X(10) X(11) X(12) X(13)
 #undef X
     default:
       return hipErrorInvalidValue;

@@ -266,7 +266,7 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
 template <int L, int MODE>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int k, int q, int set) {
-  constexpr int NT = RB<L>::NT;
+  constexpr int NT = RB<L>::NT, R = kRegAmps;
   __shared__ RBShared<L> S;
 
   const int2 it = items[blockIdx.x];
@@ -296,7 +296,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
 
   rb_stage_tables<L>(S, P, h, MODE == MODE_APPLY ? 0.0 : P.beta, tid);
 #pragma unroll
-  for (int r = 0; r < 8; ++r)
+  for (int r = 0; r < R; ++r)
     S.w[r * NT + tid] = (ab & 32) ? make_double2(1.0, 0.0) : gld(win, base + r * NT + tid);
   __syncthreads();
   rb_register_zz<L>(S, tid);
@@ -306,15 +306,15 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   // The first cross-tile flip (the rare drive in the center geometry) reads the partner tile
   // elementwise: issue those loads now so their latency hides under the sweeps.
   const bool pre = (n_fh > 0) && !(ab & 4);
-  double2 part[8];
+  double2 part[R];
   if (pre) {
     const DFlip F = S.fh[0];
     const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) part[r] = gld(src, (uint32_t)(r * NT + tid) ^ F.mask_lo);
+    for (int r = 0; r < R; ++r) part[r] = gld(src, (uint32_t)(r * NT + tid) ^ F.mask_lo);
   }
 
-  double2 out[8];
+  double2 out[R];
   rb_apply_tile_a<L>(S, P, tid, td, ab, out);
 
   if (pre) {
@@ -322,16 +322,16 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
     const bool v = par32(h & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) out[r] = cmad(out[r], cr, ci, part[r]);
+    for (int r = 0; r < R; ++r) out[r] = cmad(out[r], cr, ci, part[r]);
   }
   // epilogue operand w_{k-2}: issued now, its latency hides under the thread-pair loop
   CoefK C = {};
   if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
   const bool rd = (MODE == MODE_GEN) && !(ab & 8);
-  double2 prev[8];
+  double2 prev[R];
   if (rd) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) prev[r] = gld(wdst, base + r * NT + tid);
+    for (int r = 0; r < R; ++r) prev[r] = gld(wdst, base + r * NT + tid);
   }
 
   rb_apply_tile_b<L>(S, P, tid, ab, out);
@@ -343,7 +343,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
     const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
 #pragma unroll
-    for (int hr4 = 0; hr4 < 8; hr4 += 4) {
+    for (int hr4 = 0; hr4 < R; hr4 += 4) {
       double2 sv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr4 + r) * NT + tid) ^ F.mask_lo);
@@ -357,7 +357,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
     if (Q.mask_lo == 0u && hpar) continue;  // both bits above the tile: uniform condition
     const gd2* src = win + ((size_t)(h ^ Q.tile_xor) << L);
 #pragma unroll
-    for (int hr4 = 0; hr4 < 8; hr4 += 4) {
+    for (int hr4 = 0; hr4 < R; hr4 += 4) {
       double2 sv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) sv[r] = gld(src, (uint32_t)((hr4 + r) * NT + tid) ^ Q.mask_lo);
@@ -373,14 +373,14 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
 
   // ---- recurrence + accumulation ----
   const bool rd_acc = rd && C.upd;
-  double2 accv[8];
+  double2 accv[R];
   if (rd_acc) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) accv[r] = gld(acc_b, base + r * NT + tid);
+    for (int r = 0; r < R; ++r) accv[r] = gld(acc_b, base + r * NT + tid);
   }
   const double scale = MODE == MODE_GEN ? 2.0 * P.s1 : P.s1;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int r = 0; r < R; ++r) {
     const size_t x = base + r * NT + tid;
     const double2 own = S.w[r * NT + tid];
     if (MODE == MODE_APPLY) {

@@ -203,8 +203,7 @@ int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
       } else if (j < TB) {
         ptt.push_back(q);  // both thread bits
       } else if (i >= TB) {
-        const int a = i - TB, b = j - TB;  // both register bits: (0,1) (0,2) (1,2)
-        d.rr_g[(a == 0 && b == 1) ? 0 : (a == 0 ? 1 : 2)] = g;
+        d.rr_g[rr_index(i - TB, j - TB)] = g;  // both register bits
       } else {
         sweeps[i].g[j - TB] = g;  // thread bit i, register bit j - TB
         sweeps[i].has_pair = 1;

@@ -1,0 +1,270 @@
+"""Batched sea-detuning sweep: the GPU dispatcher behind ``run_sweep_sea_detuning``.
+
+The reference's sweep (sweep_sea_detuning.py:356-1165) loops over detunings and calls
+``simulate_rare`` three times per point, serially, writing each point's files as it goes.
+Here every (detuning, variant) evolution of the sweep is submitted at once: the evolutions
+are spread over the visible GPUs (longest-processing-time first by their Chebyshev work,
+||H|| * t_final), each GPU evolves its share concurrently inside one libdse context, and only
+then are the per-point outputs produced in detuning order, with the same file tree, names,
+keys and JSON records as the reference:
+
+    <out_root>/sea_detuning_sweep_<YYYYmmdd_HHMMSS>/
+        geometry_and_couplings.npz  global_params.json  summary.json
+        sea_detuning_report.pdf  contrast_rare_center_vs_DeltaOmega_over_geff.png
+        delta_p<...>Hz/ time_and_obs_{center_off,center_on,shell_off}.npz
+                        params_<tag>.json  freqs_<tag>.json  metrics.json  4 x PNG
+
+(:483-502, :677-685, :791, :814-1049, :1143-1157).  The plots and the PDF are produced on the
+host after the GPU work (``report="full"``, the reference's content), only the PNGs
+(``report="png"``) or not at all (``report="none"``); their time is reported separately from
+the evolution time in ``timings``.
+
+There is no CPU fallback: the evolutions run through libdse or the call raises.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import json
+import os
+import threading
+import time
+from dataclasses import asdict, replace
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .metrics import coupling_stats, point_metrics
+from .model import (DipolarRareParams, dipolar_couplings_from_positions, get_derived_frequencies,
+                    shell_positions_with_rare_center)
+from .problem import OBS_NAMES, build_problem, spectral_bounds, time_grid
+from .sweep import VARIANTS, detuning_label, f1R_for_resonance
+
+Trace = Tuple[np.ndarray, Dict[str, np.ndarray]]
+
+
+# ------------------------------------------------------------------------------------------
+# multi-GPU evolution of many parameter sets
+# ------------------------------------------------------------------------------------------
+def _visible_devices() -> List[int]:
+    from .engine import device_count
+    n = device_count()
+    if n <= 0:
+        raise RuntimeError("no HIP device visible: the sweep runs on MI355X GPUs only")
+    return list(range(n))
+
+
+def assign_lpt(costs: Sequence[float], n_bins: int) -> List[List[int]]:
+    """Longest-processing-time-first assignment of jobs to ``n_bins`` devices."""
+    bins: List[List[int]] = [[] for _ in range(n_bins)]
+    load = [0.0] * n_bins
+    for i in sorted(range(len(costs)), key=lambda k: (-costs[k], k)):
+        b = min(range(n_bins), key=lambda k: (load[k], k))
+        bins[b].append(i)
+        load[b] += costs[i]
+    for b in bins:
+        b.sort()
+    return bins
+
+
+def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequence[int]] = None,
+                tol: float = 1e-14) -> List[Trace]:
+    """``simulate_rare`` for every parameter set, spread over ``devices`` (one host thread and one
+    libdse context per GPU; the ctypes call releases the GIL).  Results in input order."""
+    grids = [time_grid(p) for p in params_list]
+    probs = [build_problem(p, order="engine", reduce=True) for p in params_list]
+    devices = list(devices) if devices is not None else _visible_devices()
+    costs = []
+    for p, pr in zip(params_list, probs):
+        lo, hi = spectral_bounds(pr)
+        costs.append(0.5 * (hi - lo) * float(p.t_final) + 30.0 * int(p.steps))
+    shares = assign_lpt(costs, len(devices))
+    results: List[Optional[Trace]] = [None] * len(params_list)
+    errors: List[BaseException] = []
+
+    def work(dev: int, idxs: List[int]) -> None:
+        from .engine import Engine
+        try:
+            with Engine(dev) as eng:
+                by_grid: Dict[Tuple[float, int], List[int]] = {}
+                for i in idxs:
+                    by_grid.setdefault((float(params_list[i].t_final), int(params_list[i].steps)),
+                                       []).append(i)
+                for group in by_grid.values():
+                    eng.clear()
+                    for i in group:
+                        eng.add(probs[i])
+                    t = grids[group[0]]
+                    obs, _ = eng.evolve(t, tol=tol)
+                    for slot, i in enumerate(group):
+                        results[i] = (t.copy(), {name: obs[slot, j].copy()
+                                                 for j, name in enumerate(OBS_NAMES)})
+        except BaseException as exc:  # re-raised in the caller's thread
+            errors.append(exc)
+
+    threads = [threading.Thread(target=work, args=(d, s)) for d, s in zip(devices, shares) if s]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    if errors:
+        raise errors[0]
+    return results  # type: ignore[return-value]
+
+
+# ------------------------------------------------------------------------------------------
+# output tree
+# ------------------------------------------------------------------------------------------
+def _json_dump(path: str, obj: Any) -> None:
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump(obj, f, indent=2, default=float)
+
+
+def _sweep_base_params(n_sea, gamma_sea, gamma_rare, B0, B1_sea, B1_rare, omega_rf_sea,
+                       omega_rf_rare, phi_sea, phi_rare, dipolar_scale, shell_scale, t_final,
+                       steps, is_spin_three_half, solver) -> DipolarRareParams:
+    """The per-detuning base record of sweep_sea_detuning.py:631-657."""
+    return DipolarRareParams(
+        n_sea=n_sea, gamma_sea=gamma_sea, gamma_rare=gamma_rare, B0_sea=B0, B0_rare=B0,
+        B1_sea=B1_sea, B1_rare=B1_rare, omega_rf_sea=omega_rf_sea, omega_rf_rare=omega_rf_rare,
+        phi_sea=phi_sea, phi_rare=phi_rare, dipolar_scale=dipolar_scale, shell_scale=shell_scale,
+        t_final=t_final, steps=steps, drive_sea=True, drive_rare=False, init_x_sign=-1,
+        init_rare_level=3, is_spin_three_half=is_spin_three_half, is_center_rare=True, **solver)
+
+
+def _variant(base: DipolarRareParams, tag: str) -> DipolarRareParams:
+    """:660-668"""
+    if tag == "center_off":
+        return replace(base, drive_rare=False, is_center_rare=True)
+    if tag == "center_on":
+        return replace(base, drive_rare=True, is_center_rare=True)
+    return replace(base, drive_rare=False, is_center_rare=False)
+
+
+def run_sweep_sea_detuning(
+    *,
+    f_Az: float,
+    f1A: float,
+    target_sea_detuning: float,
+    gamma_sea: float,
+    gamma_rare: float,
+    sea_detunings_Hz: Sequence[float],
+    n_sea: int = 12,
+    t_final: float = 3.0e-2,
+    steps: int = 2000,
+    phi_sea: float = 0.0,
+    phi_rare: float = 0.0,
+    out_root: str = "results",
+    is_spin_three_half: bool = False,
+    solver_atol: float | None = None,
+    solver_rtol: float | None = None,
+    solver_nsteps: int | None = None,
+    solver_max_step: float | None = None,
+    coarse_window: int = 50,
+    devices: Optional[Sequence[int]] = None,
+    report: str = "full",
+    timings: Optional[Dict[str, float]] = None,
+    verbose: bool = True,
+) -> str:
+    """Same arguments, outputs and return value (the sweep directory) as
+    sweep_sea_detuning.py:356-1165, plus ``devices`` (GPU ids, default all visible),
+    ``report`` ("full" | "png" | "none") and ``timings`` (filled with evolve_s / outputs_s /
+    report_s)."""
+    if report not in ("full", "png", "none"):
+        raise ValueError(f"report must be 'full', 'png' or 'none', not {report!r}")
+    say = print if verbose else (lambda *a, **k: None)
+    f1R = f1R_for_resonance(f1A, target_sea_detuning, 0.0)
+    dets = np.asarray(sea_detunings_Hz, dtype=float)
+    B0 = 2 * np.pi * f_Az / gamma_sea
+    f_Rz = gamma_rare * B0 / (2 * np.pi)
+    B1_sea = 2 * np.pi * f1A / gamma_sea
+    B1_rare = 2 * np.pi * f1R / gamma_rare if gamma_rare != 0.0 else 0.0
+    dipolar_scale = 1.0e-7 * 1.054571817e-34       # mu0/4pi * hbar (:434-436)
+    shell_scale = 0.282393e-9                      # (:437)
+
+    positions = shell_positions_with_rare_center(n_sea=n_sea, radius=shell_scale)
+    b = dipolar_couplings_from_positions(positions=positions, scale=dipolar_scale,
+                                         gamma_sea=gamma_sea, gamma_rare=gamma_rare)
+    cs = coupling_stats(b, n_sea)
+    say("Estimated dipolar couplings from geometry + physical scales:")
+    for name, key, rms in (("Sea–rare b_ij (all sea ↔ rare)", "sea_rare_abs_Hz", "sea_rare_rms_Hz"),
+                           ("Sea–sea b_ij (all i<j)", "sea_sea_abs_Hz", "sea_sea_rms_Hz")):
+        a = cs[key]
+        say(f"  {name}, |b| in Hz: avg {a.mean():.2f}  rms {cs[rms]:.2f}  "
+            f"min {a.min():.2f}  max {a.max():.2f}")
+
+    base_dir = os.path.join(out_root, "sea_detuning_sweep_"
+                            + _dt.datetime.now().strftime("%Y%m%d_%H%M%S"))
+    os.makedirs(base_dir, exist_ok=True)
+    np.savez(os.path.join(base_dir, "geometry_and_couplings.npz"), positions=positions, b=b,
+             sea_indices=np.array(list(range(n_sea)), dtype=int), idx_rare=int(n_sea),
+             sea_rare_vals=cs["sea_rare_vals"], sea_sea_vals=cs["sea_sea_vals"])
+    solver = dict(solver_atol=solver_atol, solver_rtol=solver_rtol, solver_nsteps=solver_nsteps,
+                  solver_max_step=solver_max_step)
+    global_params = {
+        "f_Az_Hz": float(f_Az), "f_Rz_Hz": float(f_Rz), "f1A_Hz": float(f1A), "f1R_Hz": float(f1R),
+        "gamma_sea": float(gamma_sea), "gamma_rare": float(gamma_rare),
+        "B0_common_T": float(B0), "B1_sea_T": float(B1_sea), "B1_rare_T": float(B1_rare),
+        "dipolar_scale_SI": float(dipolar_scale), "shell_scale_m": float(shell_scale),
+        "t_final_s": float(t_final), "steps": int(steps), "n_sea": int(n_sea),
+        "phi_sea_rad": float(phi_sea), "phi_rare_rad": float(phi_rare),
+        "sea_detunings_Hz": [float(x) for x in dets], "sea_spin_type": "1/2",
+        "rare_spin_type": "3/2" if is_spin_three_half else "1/2",
+        **solver,
+        "target_sea_detuning": target_sea_detuning, "coarse_window": int(coarse_window),
+        "avg_b_AR_Hz": float(cs["sea_rare_abs_Hz"].mean()),
+        "rms_b_AR_Hz": float(cs["sea_rare_rms_Hz"]),
+        "avg_b_AA_Hz": float(cs["sea_sea_abs_Hz"].mean()),
+        "rms_b_AA_Hz": float(cs["sea_sea_rms_Hz"]),
+    }
+    say(f"Sea detuning sweep: {len(dets)} points x 3 variants -> {base_dir}", flush=True)
+
+    # ---- all evolutions of the sweep at once ----
+    point_params: List[Dict[str, DipolarRareParams]] = []
+    for delta in dets:
+        f_rf_sea = f_Az - delta
+        base = _sweep_base_params(n_sea, gamma_sea, gamma_rare, B0, B1_sea, B1_rare,
+                                  2 * np.pi * f_rf_sea, 2 * np.pi * f_Rz, phi_sea, phi_rare,
+                                  dipolar_scale, shell_scale, t_final, steps, is_spin_three_half,
+                                  solver)
+        point_params.append({tag: _variant(base, tag) for tag in VARIANTS})
+    flat = [pp[tag] for pp in point_params for tag in VARIANTS]
+    t0 = time.perf_counter()
+    traces = evolve_many(flat, devices)
+    t1 = time.perf_counter()
+    say(f"  evolved {len(flat)} evolutions in {t1 - t0:.2f} s", flush=True)
+
+    # ---- per-point files and metrics, in detuning order ----
+    summary: Dict[str, Any] = {"global_params": global_params, "sweep_results": []}
+    details = []
+    for idx, delta in enumerate(dets):
+        det_dir = os.path.join(base_dir, detuning_label(delta))
+        os.makedirs(det_dir, exist_ok=True)
+        per = {}
+        for j, tag in enumerate(VARIANTS):
+            t_arr, obs = traces[3 * idx + j]
+            p = point_params[idx][tag]
+            np.savez(os.path.join(det_dir, f"time_and_obs_{tag}.npz"), t=t_arr, **obs)
+            _json_dump(os.path.join(det_dir, f"params_{tag}.json"), asdict(p))
+            _json_dump(os.path.join(det_dir, f"freqs_{tag}.json"), get_derived_frequencies(p))
+            per[tag] = (t_arr, obs)
+        metrics, det = point_metrics(delta, f_Az - delta, f1A, f1R, cs["sea_rare_rms_Hz"],
+                                     {k: (v[0], v[1]["Iz_sea"]) for k, v in per.items()},
+                                     coarse_window)
+        _json_dump(os.path.join(det_dir, "metrics.json"), metrics)
+        summary["sweep_results"].append(metrics)
+        details.append((det_dir, per, metrics, det))
+    t2 = time.perf_counter()
+
+    if report != "none":
+        from . import report as rep
+        rep.write_sweep_report(base_dir, global_params, summary["sweep_results"], details,
+                               pdf=(report == "full"))
+    t3 = time.perf_counter()
+
+    _json_dump(os.path.join(base_dir, "global_params.json"), summary["global_params"])
+    _json_dump(os.path.join(base_dir, "summary.json"), summary)
+    if timings is not None:
+        timings.update(evolve_s=t1 - t0, outputs_s=t2 - t1, report_s=t3 - t2)
+    say(f"Sweep complete: {base_dir} (evolve {t1 - t0:.2f} s, files {t2 - t1:.2f} s, "
+        f"report {t3 - t2:.2f} s)", flush=True)
+    return base_dir

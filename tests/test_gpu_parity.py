@@ -234,7 +234,7 @@ def test_simulate_rare_drop_in_contract():
         simulate_rare(dataclasses.replace(p, steps=1))
 
 
-@pytest.mark.parametrize("n,tile_bits", [(10, 9), (12, 12), (13, 12), (14, 13)])
+@pytest.mark.parametrize("n,tile_bits", [(11, 10), (12, 12), (13, 12), (14, 13)])
 def test_persistent_matches_streaming_and_expm(engine, n, tile_bits):
     """The persistent interval kernel (1- and 2-tile registers, cross-tile hand-off) reproduces
     the per-term streaming kernels and scipy's expm_multiply."""
