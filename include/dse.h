@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 2
+#define DSE_ABI_VERSION 3
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -123,6 +123,32 @@ int dse_add_problem(dse_ctx* ctx, int n_qubits, const double* field, const doubl
                     uint64_t sea_mask, int rare_bit, double rare_z_const);
 int dse_num_problems(const dse_ctx* ctx);
 int dse_clear(dse_ctx* ctx);
+
+/* ---- partitioned registers (SURVEY.md §8(e), configs with N >= 28) ----------------------------
+ * A register whose top shard_bits (1..3) qubits are "global": shard r holds the 2^(n-shard_bits)
+ * amplitudes whose global bits equal r.  Same tables as dse_add_problem.
+ *   shard_rank = -1  all 2^shard_bits shards in this context (one device); terms that cross
+ *                    shards read the partner shard's buffers directly.  Returns the id of shard 0;
+ *                    the other shards take the next ids.  Every shard's row of obs_out holds the
+ *                    observables of the whole register; dse_apply_h / dse_observables /
+ *                    dse_get_state on shard 0 take and return the whole 2^n state.
+ *   shard_rank >= 0  this context holds shard shard_rank of a register partitioned over
+ *                    processes (one per GPU, rank = shard_rank, world = 2^shard_bits) joined by
+ *                    dse_dist_init; before every Chebyshev term the shards that terms couple
+ *                    exchange their current vector with RCCL send/recv, and the observable sums
+ *                    are all-reduced.  dse_get_state returns the local shard (2^(n-shard_bits)).
+ * No reference counterpart: replaces QuTiP's single-process CSR product at sizes it cannot hold. */
+int dse_add_problem_sharded(dse_ctx* ctx, int n_qubits, const double* field, const double* zz,
+                            const double* pair, const double* flip, double shift,
+                            uint64_t psi0_index, uint64_t sea_mask, int rare_bit,
+                            double rare_z_const, int shard_bits, int shard_rank);
+/* RCCL bootstrap: rank 0 creates the id (DSE_DIST_ID_BYTES bytes), every rank passes it to
+ * dse_dist_init with its rank and the world size (out-of-band broadcast, e.g. torch.distributed). */
+#define DSE_DIST_ID_BYTES 128
+int dse_dist_unique_id(unsigned char* id_out);
+int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id);
+/* Local state size (amplitudes) of a problem: 2^n, or 2^(n - shard_bits) for a dist shard. */
+int64_t dse_problem_dim(const dse_ctx* ctx, int problem);
 
 /* ---- hot path ----------------------------------------------------------------------------- */
 /* psi_out = H psi_in for one problem (interleaved complex, 2^n each).  Test/diagnostic hook:

@@ -44,7 +44,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-Wno-unused-result",
            "-I", os.path.join(ROOT, "include"),
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
+           *[os.path.join(CSRC, s) for s in SOURCES],
+           "-L", "/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)

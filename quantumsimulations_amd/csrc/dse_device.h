@@ -31,6 +31,7 @@ typedef double __attribute__((ext_vector_type(2))) dv2;
 typedef __attribute__((address_space(1))) dv2 gd2;
 typedef __attribute__((address_space(1))) double gdbl;
 __device__ __forceinline__ gd2* gptr(double2* p) { return (gd2*)p; }
+__device__ __forceinline__ const gd2* gptr(const double2* p) { return (const gd2*)p; }
 __device__ __forceinline__ const gdbl* gptr(const double* p) { return (const gdbl*)p; }
 __device__ __forceinline__ double2 gld(const gd2* p, size_t i) {
   const dv2 v = p[i];

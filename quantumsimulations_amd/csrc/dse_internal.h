@@ -19,6 +19,8 @@ constexpr int kRegBlockMinTile = 6 + kRegBits;    // tiles >= 2^10 (>= one wave)
 __host__ __device__ constexpr int rr_index(int a, int b) {
   return a * (2 * kRegBits - a - 1) / 2 + (b - a - 1);
 }
+constexpr int kMaxShardBits = 3;                  // partitioned registers: up to 8 shards
+constexpr int kMaxShards = 1 << kMaxShardBits;
 // bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index
 #define DSE_MAX_HIGH_BITS(L) ((34 - (L)) < 0 ? 0 : (34 - (L)))
 
@@ -83,7 +85,21 @@ struct DevProb {
   int rare_bit;
   int n_sea;
   int rflip_mask;         // bit i set: register bit i has a drive flip
+  // Partitioned registers (dse_add_problem_sharded): this problem holds shard `rank` of a
+  // register whose top `shard_bits` qubits are global.  Tile indices in the kernels are global
+  // (hg = h_base | h for local tile h); a tile of shard rank ^ m is read through rbuf[m][role]
+  // (the partner's own buffers on the same device, or receive buffers filled by an exchange).
+  uint32_t h_base;        // rank << tbl (0 for an ordinary problem)
+  int tbl;                // local tile-index bits: log2(tiles of this shard)
+  double2* rbuf[kMaxShards][3];
 };
+
+// Global tile hp of the role-`role` vector: local buffer or a partner shard's.
+__device__ __forceinline__ const double2* tile_ptr(const DevProb& P, int role, uint32_t hp) {
+  const uint32_t gm = (hp ^ P.h_base) >> P.tbl;
+  const double2* b = gm ? P.rbuf[gm][role] : P.buf[role];
+  return b + ((size_t)(hp & ((1u << P.tbl) - 1u)) << P.L);
+}
 
 hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items, int n_items,
                        int k, int q, int set, hipStream_t st);

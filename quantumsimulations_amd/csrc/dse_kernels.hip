@@ -35,7 +35,8 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
 
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
-  const uint32_t h = (uint32_t)it.y;
+  const uint32_t h = (uint32_t)it.y;       // local tile
+  const uint32_t hg = P.h_base | h;          // global tile index (partitioned registers)
   const int tid = threadIdx.x;
   const bool live = (T >= NT) || (tid < T);
   if (MODE == MODE_GEN && k > P.degree) return;  // uniform: this problem's interval is done
@@ -44,18 +45,19 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
   double2* psi_b = P.buf[q ? 2 : 0];
   double2* acc_b = P.buf[q ? 0 : 2];
   double2* scr_b = P.buf[1];
-  const double2* win;
+  int win_role;
   double2* wdst;
   if (MODE == MODE_APPLY) {
-    win = P.buf[0];
+    win_role = 0;
     wdst = P.buf[1];
   } else if (MODE == MODE_FIRST) {
-    win = psi_b;
+    win_role = q ? 2 : 0;
     wdst = scr_b;
   } else {
-    win = ((k - 1) & 1) ? scr_b : psi_b;
+    win_role = ((k - 1) & 1) ? 1 : (q ? 2 : 0);
     wdst = (k & 1) ? scr_b : psi_b;  // holds w_{k-2}; overwritten in place with w_k
   }
+  const double2* win = P.buf[win_role];
   const size_t base = (size_t)h << L;
 
   double2 own[R];
@@ -67,7 +69,7 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
       s_w[x] = own[r];
     }
   }
-  tile_diag_coeffs<L>(P, h, MODE == MODE_APPLY ? 0.0 : P.beta, s_c, tid);
+  tile_diag_coeffs<L>(P, hg, MODE == MODE_APPLY ? 0.0 : P.beta, s_c, tid);
   __syncthreads();
   if (!live) return;
 
@@ -113,9 +115,9 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
   // ---- terms reaching other tiles (global, L2-served) ----
   for (int f = 0; f < P.n_flips_hi; ++f) {
     const DFlip F = P.flips_hi[f];
-    const bool v = par32(h & F.tile_xor);
+    const bool v = par32(hg & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
-    const double2* src = win + ((size_t)(h ^ F.tile_xor) << L);
+    const double2* src = tile_ptr(P, win_role, hg ^ F.tile_xor);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const uint32_t x = (uint32_t)(r * NT + tid);
@@ -124,8 +126,8 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
   }
   for (int p = 0; p < P.n_pairs_hi; ++p) {
     const DPair Q = P.pairs_hi[p];
-    const int hp = par32(h & Q.tile_xor);
-    const double2* src = win + ((size_t)(h ^ Q.tile_xor) << L);
+    const int hp = par32(hg & Q.tile_xor);
+    const double2* src = tile_ptr(P, win_role, hg ^ Q.tile_xor);
     if (Q.mask_lo == 0u) {
       if (hp) continue;  // both bits above the tile: uniform condition
 #pragma unroll
@@ -171,6 +173,7 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
   const uint32_t h = (uint32_t)it.y;
+  const uint32_t hg = P.h_base | h;
   const int tid = threadIdx.x;
   const bool live = (T >= NT) || (tid < T);
   const double2* psi = P.buf[bsel];
@@ -189,7 +192,7 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
 
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};
   if (live) {
-    const uint64_t hi = (uint64_t)h << L;
+    const uint64_t hi = (uint64_t)hg << L;
     const double half_sea = 0.5 * (double)P.n_sea;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -215,8 +218,8 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
           }
         }
       } else {
-        if ((h >> (b - L)) & 1u) continue;
-        const double2* src = psi + ((size_t)(h ^ (1u << (b - L))) << L);
+        if ((hg >> (b - L)) & 1u) continue;
+        const double2* src = tile_ptr(P, bsel, hg ^ (1u << (b - L)));
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const double2 s = src[r * NT + tid];
@@ -271,7 +274,8 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
 
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
-  const uint32_t h = (uint32_t)it.y;
+  const uint32_t h = (uint32_t)it.y;       // local tile
+  const uint32_t hg = P.h_base | h;          // global tile index (partitioned registers)
   const int tid = threadIdx.x;
   if (MODE == MODE_GEN && k > P.degree) return;  // uniform: this problem's interval is done
 
@@ -280,21 +284,22 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   gd2* psi_b = gptr(P.buf[q ? 2 : 0]);
   gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
   gd2* scr_b = gptr(P.buf[1]);
-  const gd2* win;
+  int win_role;
   gd2* wdst;
   if (MODE == MODE_APPLY) {
-    win = gptr(P.buf[0]);
+    win_role = 0;
     wdst = gptr(P.buf[1]);
   } else if (MODE == MODE_FIRST) {
-    win = psi_b;
+    win_role = q ? 2 : 0;
     wdst = scr_b;
   } else {
-    win = ((k - 1) & 1) ? scr_b : psi_b;
+    win_role = ((k - 1) & 1) ? 1 : (q ? 2 : 0);
     wdst = (k & 1) ? scr_b : psi_b;
   }
+  const gd2* win = gptr(P.buf[win_role]);
   const size_t base = (size_t)h << L;
 
-  rb_stage_tables<L>(S, P, h, MODE == MODE_APPLY ? 0.0 : P.beta, tid);
+  rb_stage_tables<L>(S, P, hg, MODE == MODE_APPLY ? 0.0 : P.beta, tid);
 #pragma unroll
   for (int r = 0; r < R; ++r)
     S.w[r * NT + tid] = (ab & 32) ? make_double2(1.0, 0.0) : gld(win, base + r * NT + tid);
@@ -309,7 +314,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   double2 part[R];
   if (pre) {
     const DFlip F = S.fh[0];
-    const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
+    const gd2* src = gptr(tile_ptr(P, win_role, hg ^ F.tile_xor));
 #pragma unroll
     for (int r = 0; r < R; ++r) part[r] = gld(src, (uint32_t)(r * NT + tid) ^ F.mask_lo);
   }
@@ -319,7 +324,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
 
   if (pre) {
     const DFlip F = S.fh[0];
-    const bool v = par32(h & F.tile_xor);
+    const bool v = par32(hg & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
 #pragma unroll
     for (int r = 0; r < R; ++r) out[r] = cmad(out[r], cr, ci, part[r]);
@@ -339,9 +344,9 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   // ---- remaining cross-tile terms (global, L2/MALL-served), four registers at a time ----
   for (int f = 1; f < ((ab & 4) ? 0 : n_fh); ++f) {
     const DFlip F = S.fh[f];
-    const bool v = par32(h & F.tile_xor);
+    const bool v = par32(hg & F.tile_xor);
     const double cr = v ? F.re1 : F.re0, ci = v ? F.im1 : F.im0;
-    const gd2* src = win + ((size_t)(h ^ F.tile_xor) << L);
+    const gd2* src = gptr(tile_ptr(P, win_role, hg ^ F.tile_xor));
 #pragma unroll
     for (int hr4 = 0; hr4 < R; hr4 += 4) {
       double2 sv[4];
@@ -353,9 +358,9 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   }
   for (int p = 0; p < ((ab & 4) ? 0 : n_ph); ++p) {
     const DPair Q = S.ph[p];
-    const int hpar = par32(h & Q.tile_xor);
+    const int hpar = par32(hg & Q.tile_xor);
     if (Q.mask_lo == 0u && hpar) continue;  // both bits above the tile: uniform condition
-    const gd2* src = win + ((size_t)(h ^ Q.tile_xor) << L);
+    const gd2* src = gptr(tile_ptr(P, win_role, hg ^ Q.tile_xor));
 #pragma unroll
     for (int hr4 = 0; hr4 < R; hr4 += 4) {
       double2 sv[4];

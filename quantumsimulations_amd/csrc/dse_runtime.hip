@@ -24,6 +24,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/dse.h"
 #include "dse_internal.h"
 
@@ -49,6 +51,13 @@ struct HostProblem {
   int degree = 1;
   double flops_per_amp = 0.0;  // algorithmic flops of one H application per amplitude
   int2* d_items = nullptr;  // this problem's tiles (apply_h / observables hooks)
+  // partitioned register (dse_add_problem_sharded): shard `shard_rank` of 2^shard_bits
+  int shard_bits = 0, shard_rank = 0;
+  int n_local = 0;           // qubits held by this shard (n - shard_bits)
+  int group_first = -1;      // loopback group: index of shard 0 (all shards in this context)
+  bool dist = false;         // shard of a register partitioned over processes (RCCL exchange)
+  uint32_t xmasks = 0;       // bit m set: terms or observables read shard rank ^ m
+  double2* rbuf_own[kMaxShards] = {};  // dist: receive buffers of the exchange, per mask
 };
 
 // One stream's share of the problems, grouped by tile size.
@@ -96,6 +105,9 @@ struct dse_ctx {
   int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
   double max_degree = 2e6;
+  // partitioned registers over processes: one RCCL communicator, one rank per GPU
+  ncclComm_t comm = nullptr;
+  int dist_rank = 0, dist_world = 1;
 };
 
 namespace {
@@ -123,6 +135,8 @@ void free_device(dse_ctx* ctx) {
     if (p.tables) (void)hipFree(p.tables), p.tables = nullptr;
     if (p.coef) (void)hipFree(p.coef), p.coef = nullptr;
     if (p.d_items) (void)hipFree(p.d_items), p.d_items = nullptr;
+    for (auto& b : p.rbuf_own)
+      if (b) (void)hipFree(b), b = nullptr;
     p.coef_bytes = 0;
   }
   if (ctx->d_probs) (void)hipFree(ctx->d_probs), ctx->d_probs = nullptr;
@@ -164,10 +178,11 @@ int sync_all(dse_ctx* ctx) {
 // ---- per-problem device tables ------------------------------------------------------------
 int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
   const int n = p.n;
-  const int L = std::max(std::min(n, ctx->tile_bits), std::max(kMinTile, n - 32));
+  const int nl = p.n_local;   // qubits held in this context (n unless partitioned)
+  const int L = std::max(std::min(nl, ctx->tile_bits), std::max(kMinTile, nl - 32));
   if (L > kMaxTile) return fail(ctx, DSE_ERR_ARG, "problem too large for the tile range");
   p.L = L;
-  p.n_tiles = int64_t(1) << (n - L);
+  p.n_tiles = int64_t(1) << (nl - L);
   const size_t T = size_t(1) << L;
   const uint64_t lo_mask = (uint64_t(1) << L) - 1;
   const bool rb = L >= kRegBlockMinTile;
@@ -262,7 +277,7 @@ int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
   if (hipMalloc(&p.tables, total) != hipSuccess)
     return fail(ctx, DSE_ERR_OOM, "device allocation of coefficient tables failed");
   HIPC(hipMemcpy(p.tables, blob.data(), total, hipMemcpyHostToDevice));
-  const size_t vbytes = (size_t(1) << n) * sizeof(double2);
+  const size_t vbytes = (size_t(1) << nl) * sizeof(double2);
   for (auto& b : p.buf) {
     if (hipMalloc(&b, vbytes) != hipSuccess)
       return fail(ctx, DSE_ERR_OOM, "device allocation of state buffers failed (" +
@@ -303,6 +318,18 @@ int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
   d.kcap1 = 0;
   d.rare_bit = p.rare_bit;
   d.n_sea = __builtin_popcountll(p.sea_mask);
+  // partitioned register: global tile index = rank << tbl | local tile; partner masks
+  d.tbl = nl - L;
+  d.h_base = (uint32_t)p.shard_rank << d.tbl;
+  p.xmasks = 0;
+  if (p.shard_bits > 0) {
+    for (const auto& q : phi)
+      if (q.tile_xor >> d.tbl) p.xmasks |= 1u << (q.tile_xor >> d.tbl);
+    for (const auto& q : fhi)
+      if (q.tile_xor >> d.tbl) p.xmasks |= 1u << (q.tile_xor >> d.tbl);
+    for (int b = nl; b < n; ++b)  // <Ix>, <Iy> of a global qubit pair amplitudes across shards
+      if (((p.sea_mask >> b) & 1ull) || b == p.rare_bit) p.xmasks |= 1u << (1u << (b - nl));
+  }
   return DSE_OK;
 }
 
@@ -327,6 +354,25 @@ int prepare(dse_ctx* ctx) {
     }
     HIPC(hipMemcpy(p.d_items, its.data(), its.size() * sizeof(int2), hipMemcpyHostToDevice));
     total += p.n_tiles;
+  }
+  // partitioned registers: partner shards' buffers (same context) or exchange receive buffers
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    HostProblem& p = ctx->probs[pi];
+    if (p.shard_bits == 0) continue;
+    for (int m = 1; m < (1 << p.shard_bits); ++m) {
+      if (!((p.xmasks >> m) & 1u)) continue;
+      if (p.dist) {
+        const size_t vbytes = (size_t(1) << p.n_local) * sizeof(double2);
+        if (hipMalloc(&p.rbuf_own[m], vbytes) != hipSuccess) {
+          free_device(ctx);
+          return fail(ctx, DSE_ERR_OOM, "device allocation of exchange buffers failed");
+        }
+        for (int r = 0; r < 3; ++r) dp[pi].rbuf[m][r] = p.rbuf_own[m];
+      } else {
+        const HostProblem& q = ctx->probs[p.group_first + (p.shard_rank ^ m)];
+        for (int r = 0; r < 3; ++r) dp[pi].rbuf[m][r] = q.buf[r];
+      }
+    }
   }
   if (hipMalloc(&ctx->d_probs, dp.size() * sizeof(DevProb)) != hipSuccess ||
       hipMalloc(&ctx->d_items, total * sizeof(int2)) != hipSuccess) {
@@ -362,20 +408,57 @@ void finish_obs(const HostProblem& P, const double* v, double* o, size_t stride)
   o[6 * stride] = std::sqrt(n2);
 }
 
-int flush_partials(dse_ctx* ctx, size_t nslots, size_t t0, int n_t, double* obs_out) {
+// Observable sums of output slots [t0, t0 + nslots).  A loopback shard group sums the tiles of all
+// its shards and writes the result to every shard's row; a dist shard keeps its raw local sums in
+// dist_raw for the all-reduce at the end of dse_evolve.
+int flush_partials(dse_ctx* ctx, size_t nslots, size_t t0, int n_t, double* obs_out,
+                   std::vector<double>* dist_raw) {
   if ((int)sync_all(ctx)) return DSE_ERR_HIP;
   std::vector<double> h(nslots * ctx->total_items * 8);
   HIPC(hipMemcpy(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost));
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     const HostProblem& P = ctx->probs[pi];
-    const int64_t first = ctx->item_pos[pi];
+    const bool grouped = P.shard_bits > 0 && !P.dist;
+    const size_t first_member = grouped ? (size_t)P.group_first : pi;
+    const size_t n_members = grouped ? (size_t(1) << P.shard_bits) : 1;
     for (size_t s = 0; s < nslots; ++s) {
       double v[7] = {0, 0, 0, 0, 0, 0, 0};
-      const double* row = h.data() + (s * ctx->total_items + first) * 8;
-      for (int64_t t = 0; t < P.n_tiles; ++t)
-        for (int j = 0; j < 7; ++j) v[j] += row[t * 8 + j];
-      finish_obs(P, v, obs_out + pi * DSE_N_OBS * (size_t)n_t + (t0 + s), (size_t)n_t);
+      for (size_t mi = first_member; mi < first_member + n_members; ++mi) {
+        const double* row = h.data() + (s * ctx->total_items + ctx->item_pos[mi]) * 8;
+        for (int64_t t = 0; t < ctx->probs[mi].n_tiles; ++t)
+          for (int j = 0; j < 7; ++j) v[j] += row[t * 8 + j];
+      }
+      if (P.dist) {
+        double* raw = dist_raw->data() + (pi * (size_t)n_t + t0 + s) * 7;
+        for (int j = 0; j < 7; ++j) raw[j] = v[j];
+      } else {
+        finish_obs(P, v, obs_out + pi * DSE_N_OBS * (size_t)n_t + (t0 + s), (size_t)n_t);
+      }
     }
+  }
+  return DSE_OK;
+}
+
+// RCCL exchange for dist shards: every shard sends its role-`role` vector to each partner rank ^ m
+// it shares terms with and receives the partner's into rbuf_own[m] (min_degree: only problems
+// whose Chebyshev degree reaches the current term).
+int dist_exchange(dse_ctx* ctx, int role, int min_degree, hipStream_t st) {
+  for (auto& P : ctx->probs) {
+    if (!P.dist || P.degree < min_degree || !P.xmasks) continue;
+    const size_t bytes = (size_t(1) << P.n_local) * sizeof(double2);
+    if (ncclGroupStart() != ncclSuccess) return fail(ctx, DSE_ERR_HIP, "ncclGroupStart failed");
+    for (int m = 1; m < (1 << P.shard_bits); ++m) {
+      if (!((P.xmasks >> m) & 1u)) continue;
+      const int peer = ctx->dist_rank ^ m;
+      ncclResult_t r1 = ncclSend(P.buf[role], bytes, ncclUint8, peer, ctx->comm, st);
+      ncclResult_t r2 = ncclRecv(P.rbuf_own[m], bytes, ncclUint8, peer, ctx->comm, st);
+      if (r1 != ncclSuccess || r2 != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return fail(ctx, DSE_ERR_HIP, std::string("RCCL send/recv: ") + ncclGetErrorString(r1 != ncclSuccess ? r1 : r2));
+      }
+    }
+    const ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(r));
   }
   return DSE_OK;
 }
@@ -444,6 +527,7 @@ void dse_destroy(dse_ctx* ctx) {
   (void)sync_all(ctx);
   free_device(ctx);
   destroy_lanes(ctx);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   delete ctx;
 }
 
@@ -485,17 +569,20 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   return DSE_OK;
 }
 
-int dse_add_problem(dse_ctx* ctx, int n, const double* field, const double* zz, const double* pair,
-                    const double* flip, double shift, uint64_t psi0_index, uint64_t sea_mask,
-                    int rare_bit, double rare_z_const) {
-  if (!ctx) return DSE_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+// Validated host copy of one problem's tables (dse_add_problem / dse_add_problem_sharded).
+int make_problem(dse_ctx* ctx, HostProblem& p, int n, const double* field, const double* zz,
+                 const double* pair, const double* flip, double shift, uint64_t psi0_index,
+                 uint64_t sea_mask, int rare_bit, double rare_z_const) {
   if (n < 1 || n > DSE_MAX_QUBITS) return fail(ctx, DSE_ERR_ARG, "n_qubits out of range 1..34");
   if (!field || !zz || !pair || !flip) return fail(ctx, DSE_ERR_ARG, "null coefficient table");
   const uint64_t dim = uint64_t(1) << n;
   if (psi0_index >= dim) return fail(ctx, DSE_ERR_ARG, "psi0_index >= 2^n");
   if ((sea_mask >> n) != 0) return fail(ctx, DSE_ERR_ARG, "sea_mask has bits >= n");
   if (rare_bit >= n || rare_bit < -1) return fail(ctx, DSE_ERR_ARG, "rare_bit out of range");
-  HostProblem p;
   p.n = n;
   p.field.assign(field, field + n);
   p.zz.assign(zz, zz + size_t(n) * n);
@@ -521,6 +608,7 @@ int dse_add_problem(dse_ctx* ctx, int n, const double* field, const double* zz, 
   p.sea_mask = sea_mask;
   p.rare_bit = rare_bit;
   p.rare_z = rare_z_const;
+  p.n_local = n;
   dse_spectral_bounds(n, p.field.data(), p.zz.data(), p.pair.data(), p.flip.data(), shift, &p.e_min, &p.e_max);
   {  // diagonal 4, drive flip 8 (complex coefficient), pair 4 on the half of the rows where it acts
     double f = 4.0;
@@ -531,11 +619,99 @@ int dse_add_problem(dse_ctx* ctx, int n, const double* field, const double* zz, 
         if (p.pair[i * n + j] != 0.0) f += 2.0;
     p.flops_per_amp = f;
   }
+  return DSE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dse_add_problem(dse_ctx* ctx, int n, const double* field, const double* zz, const double* pair,
+                    const double* flip, double shift, uint64_t psi0_index, uint64_t sea_mask,
+                    int rare_bit, double rare_z_const) {
+  if (!ctx) return DSE_ERR_ARG;
+  HostProblem p;
+  int rc = make_problem(ctx, p, n, field, zz, pair, flip, shift, psi0_index, sea_mask, rare_bit,
+                        rare_z_const);
+  if (rc) return rc;
   (void)hipSetDevice(ctx->device);
   (void)sync_all(ctx);
   free_device(ctx);  // device layout is rebuilt lazily
   ctx->probs.push_back(std::move(p));
   return (int)ctx->probs.size() - 1;
+}
+
+int dse_add_problem_sharded(dse_ctx* ctx, int n, const double* field, const double* zz,
+                            const double* pair, const double* flip, double shift,
+                            uint64_t psi0_index, uint64_t sea_mask, int rare_bit,
+                            double rare_z_const, int shard_bits, int shard_rank) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (shard_bits < 1 || shard_bits > kMaxShardBits)
+    return fail(ctx, DSE_ERR_ARG, "shard_bits must be in 1..3");
+  if (shard_rank < -1 || shard_rank >= (1 << shard_bits))
+    return fail(ctx, DSE_ERR_ARG, "shard_rank out of range");
+  HostProblem p;
+  int rc = make_problem(ctx, p, n, field, zz, pair, flip, shift, psi0_index, sea_mask, rare_bit,
+                        rare_z_const);
+  if (rc) return rc;
+  if (n - shard_bits < kMinTile + 1)
+    return fail(ctx, DSE_ERR_ARG, "register too small to partition");
+  if (shard_rank >= 0 && (!ctx->comm || ctx->dist_world != (1 << shard_bits) ||
+                          ctx->dist_rank != shard_rank))
+    return fail(ctx, DSE_ERR_STATE, "dist shard needs dse_dist_init with world = 2^shard_bits "
+                                    "and rank = shard_rank");
+  p.shard_bits = shard_bits;
+  p.n_local = n - shard_bits;
+  (void)hipSetDevice(ctx->device);
+  (void)sync_all(ctx);
+  free_device(ctx);
+  const int first = (int)ctx->probs.size();
+  if (shard_rank >= 0) {
+    p.shard_rank = shard_rank;
+    p.dist = true;
+    ctx->probs.push_back(std::move(p));
+    return first;
+  }
+  for (int r = 0; r < (1 << shard_bits); ++r) {
+    HostProblem q = p;
+    q.shard_rank = r;
+    q.group_first = first;
+    ctx->probs.push_back(std::move(q));
+  }
+  return first;
+}
+
+int dse_dist_unique_id(unsigned char* id_out) {
+  if (!id_out) return DSE_ERR_ARG;
+  static_assert(sizeof(ncclUniqueId) == DSE_DIST_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return DSE_ERR_HIP;
+  std::memcpy(id_out, &id, sizeof(id));
+  return DSE_OK;
+}
+
+int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id) {
+  if (!ctx || !id) return DSE_ERR_ARG;
+  if (world < 2 || world > kMaxShards || (world & (world - 1)) || rank < 0 || rank >= world)
+    return fail(ctx, DSE_ERR_ARG, "world must be 2, 4 or 8 and 0 <= rank < world");
+  if (ctx->comm) return fail(ctx, DSE_ERR_STATE, "dse_dist_init called twice");
+  HIPC(hipSetDevice(ctx->device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  const ncclResult_t r = ncclCommInitRank(&ctx->comm, world, uid, rank);
+  if (r != ncclSuccess) {
+    ctx->comm = nullptr;
+    return fail(ctx, DSE_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  ctx->dist_rank = rank;
+  ctx->dist_world = world;
+  return DSE_OK;
+}
+
+int64_t dse_problem_dim(const dse_ctx* ctx, int problem) {
+  if (!ctx || problem < 0 || problem >= (int)ctx->probs.size()) return DSE_ERR_ARG;
+  const HostProblem& P = ctx->probs[problem];
+  return int64_t(1) << (P.dist ? P.n_local : P.n);
 }
 
 int dse_num_problems(const dse_ctx* ctx) { return ctx ? (int)ctx->probs.size() : DSE_ERR_ARG; }
@@ -549,19 +725,54 @@ int dse_clear(dse_ctx* ctx) {
   return DSE_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// The problems a hook call on `problem` acts on: the whole loopback group for its shard 0, else
+// the problem itself.  Host vectors are the whole register (group) or the local shard.
+int hook_members(dse_ctx* ctx, int problem, int* first, int* count) {
+  if (problem < 0 || problem >= (int)ctx->probs.size()) return fail(ctx, DSE_ERR_ARG, "bad problem id");
+  const HostProblem& P = ctx->probs[problem];
+  *first = problem;
+  *count = 1;
+  if (P.shard_bits > 0 && !P.dist) {
+    if (P.shard_rank != 0) return fail(ctx, DSE_ERR_ARG, "use shard 0 of a partitioned register");
+    *count = 1 << P.shard_bits;
+  }
+  return DSE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out) {
   if (!ctx) return DSE_ERR_ARG;
-  if (problem < 0 || problem >= (int)ctx->probs.size()) return fail(ctx, DSE_ERR_ARG, "bad problem id");
   if (!psi_in || !psi_out) return fail(ctx, DSE_ERR_ARG, "null state");
-  HIPC(hipSetDevice(ctx->device));
-  int rc = prepare(ctx);
+  int first = 0, count = 1;
+  int rc = hook_members(ctx, problem, &first, &count);
   if (rc) return rc;
-  HostProblem& P = ctx->probs[problem];
+  HIPC(hipSetDevice(ctx->device));
+  if ((rc = prepare(ctx))) return rc;
   hipStream_t st = ctx->lanes[0].stream;
-  const size_t bytes = (size_t(1) << P.n) * sizeof(double2);
-  HIPC(hipMemcpyAsync(P.buf[0], psi_in, bytes, hipMemcpyHostToDevice, st));
-  HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
-  HIPC(hipMemcpyAsync(psi_out, P.buf[1], bytes, hipMemcpyDeviceToHost, st));
+  const double2* in = reinterpret_cast<const double2*>(psi_in);
+  double2* out = reinterpret_cast<double2*>(psi_out);
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    const size_t amps = size_t(1) << P.n_local;
+    HIPC(hipMemcpyAsync(P.buf[0], in + i * amps, amps * sizeof(double2), hipMemcpyHostToDevice, st));
+  }
+  if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+  }
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    const size_t amps = size_t(1) << P.n_local;
+    HIPC(hipMemcpyAsync(out + i * amps, P.buf[1], amps * sizeof(double2), hipMemcpyDeviceToHost, st));
+  }
   HIPC(hipStreamSynchronize(st));
   ctx->evolved = false;
   return DSE_OK;
@@ -569,24 +780,47 @@ int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out
 
 int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) {
   if (!ctx) return DSE_ERR_ARG;
-  if (problem < 0 || problem >= (int)ctx->probs.size()) return fail(ctx, DSE_ERR_ARG, "bad problem id");
   if (!psi || !obs7) return fail(ctx, DSE_ERR_ARG, "null pointer");
-  HIPC(hipSetDevice(ctx->device));
-  int rc = prepare(ctx);
+  int first = 0, count = 1;
+  int rc = hook_members(ctx, problem, &first, &count);
   if (rc) return rc;
+  HIPC(hipSetDevice(ctx->device));
+  if ((rc = prepare(ctx))) return rc;
+  int64_t tiles = 0;
+  for (int i = 0; i < count; ++i) tiles += ctx->probs[first + i].n_tiles;
   if ((rc = ensure_partial(ctx, 1))) return rc;
-  HostProblem& P = ctx->probs[problem];
   hipStream_t st = ctx->lanes[0].stream;
-  const size_t bytes = (size_t(1) << P.n) * sizeof(double2);
-  HIPC(hipMemcpyAsync(P.buf[0], psi, bytes, hipMemcpyHostToDevice, st));
-  HIPC(launch_obs(P.L, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, ctx->d_partial, st));
-  std::vector<double> h(P.n_tiles * 8);
+  const double2* in = reinterpret_cast<const double2*>(psi);
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    const size_t amps = size_t(1) << P.n_local;
+    HIPC(hipMemcpyAsync(P.buf[0], in + i * amps, amps * sizeof(double2), hipMemcpyHostToDevice, st));
+  }
+  if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
+  int64_t off = 0;
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    HIPC(launch_obs(P.L, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, ctx->d_partial + off * 8, st));
+    off += P.n_tiles;
+  }
+  std::vector<double> h(tiles * 8);
   HIPC(hipMemcpyAsync(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
   HIPC(hipStreamSynchronize(st));
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int64_t t = 0; t < P.n_tiles; ++t)
+  for (int64_t t = 0; t < tiles; ++t)
     for (int j = 0; j < 7; ++j) v[j] += h[t * 8 + j];
-  finish_obs(P, v, obs7, 1);
+  if (ctx->probs[first].dist) {  // sum over the shards of all ranks
+    double* d = nullptr;
+    HIPC(hipMalloc(&d, 7 * sizeof(double)));
+    HIPC(hipMemcpy(d, v, 7 * sizeof(double), hipMemcpyHostToDevice));
+    const ncclResult_t r = ncclAllReduce(d, d, 7, ncclFloat64, ncclSum, ctx->comm, st);
+    hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMemcpy(v, d, 7 * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    HIPC(e);
+  }
+  finish_obs(ctx->probs[first], v, obs7, 1);
   ctx->evolved = false;
   return DSE_OK;
 }
@@ -693,9 +927,13 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   // interval and lane; 2-tile problems on lane 0 (their workgroup pairs must be co-resident),
   // 1-tile problems on lane 1.  streaming: problems by degree dealt round-robin over the lanes.
   bool persistent = ctx->persistent != 0;
-  for (auto& P : ctx->probs)
-    if (!(interval_supported(P.L) && P.n_tiles <= 2)) persistent = false;
-  const int n_lanes = std::min<int>(ctx->n_streams, (int)ctx->probs.size());
+  bool any_dist = false;
+  for (auto& P : ctx->probs) {
+    if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
+    any_dist = any_dist || P.dist;
+  }
+  // dist shards: one lane, so the RCCL exchanges are stream-ordered with every launch
+  const int n_lanes = any_dist ? 1 : std::min<int>(ctx->n_streams, (int)ctx->probs.size());
   std::vector<int> order(ctx->probs.size());
   std::iota(order.begin(), order.end(), 0);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
@@ -708,6 +946,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     const std::pair<int, int64_t> key(P.L, P.n_tiles);
     int lane = (int)(i % n_lanes);
     if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1) ? 0 : 1;
+    // shards of one register read each other's vectors: same lane, hence the same launches
+    if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);
   }
   std::vector<int2> items;
@@ -771,10 +1011,13 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   // ---- psi(t0) = |psi0> ----
   hipStream_t st0 = ctx->lanes[0].stream;
   for (auto& P : ctx->probs) {
-    const size_t vbytes = (size_t(1) << P.n) * sizeof(double2);
+    const size_t vbytes = (size_t(1) << P.n_local) * sizeof(double2);
     HIPC(hipMemsetAsync(P.buf[0], 0, vbytes, st0));
     static const double2 one = {1.0, 0.0};
-    HIPC(hipMemcpyAsync(P.buf[0] + P.psi0, &one, sizeof(double2), hipMemcpyHostToDevice, st0));
+    if ((P.psi0 >> P.n_local) == (uint64_t)P.shard_rank) {  // the shard holding psi0
+      const uint64_t local = P.psi0 & ((uint64_t(1) << P.n_local) - 1);
+      HIPC(hipMemcpyAsync(P.buf[0] + local, &one, sizeof(double2), hipMemcpyHostToDevice, st0));
+    }
   }
   HIPC(hipStreamSynchronize(st0));
 
@@ -815,7 +1058,9 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     return DSE_OK;
   };
 
+  std::vector<double> dist_raw(any_dist ? ctx->probs.size() * (size_t)n_t * 7 : 0, 0.0);
   size_t slot = 0, t_flushed = 0;
+  if (any_dist && (rc = dist_exchange(ctx, 0, 0, ctx->lanes[0].stream))) return rc;
   if ((rc = obs_all(0, slot++))) return rc;
   for (int m = 0; m + 1 < n_t; ++m) {
     const int q = m & 1;
@@ -855,10 +1100,13 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
           }
           continue;
         }
+        if (any_dist && (rc = dist_exchange(ctx, q ? 2 : 0, 1, ln.stream))) return rc;
         HIPC(launch_step(g.L, MODE_FIRST, ctx->d_probs, ctx->d_items + g.off, g.active[1], 1, q, set, ln.stream));
         for (int k = 2; k < (int)g.active.size(); ++k) {
           const int na = g.active[k];
           if (na <= 0) break;
+          if (any_dist && (rc = dist_exchange(ctx, ((k - 1) & 1) ? 1 : (q ? 2 : 0), k, ln.stream)))
+            return rc;
           if (timed) {
             const size_t i = ln.ev_used[pool]++;
             HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
@@ -877,15 +1125,16 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       }
     }
     // new psi of every problem sits in acc(q) = buf[q ? 0 : 2]
+    if (any_dist && (rc = dist_exchange(ctx, q ? 0 : 2, 0, ctx->lanes[0].stream))) return rc;
     if ((rc = obs_all(q ? 0 : 2, slot++))) return rc;
     if (slot == chunk) {
-      if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out))) return rc;
+      if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
       t_flushed += slot;
       slot = 0;
     }
   }
   if (slot > 0) {
-    if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out))) return rc;
+    if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
     t_flushed += slot;
   }
   for (size_t li = 0; li < ctx->lanes.size(); ++li)
@@ -896,6 +1145,25 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     int herr = 0;
     HIPC(hipMemcpy(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr) return fail(ctx, DSE_ERR_HIP, "cross-tile hand-off timed out (workgroup pair not co-resident)");
+  }
+  if (any_dist) {  // sums over all shards of the register, then normalisation (finish_obs)
+    double* d_raw = nullptr;
+    const size_t rb = dist_raw.size() * sizeof(double);
+    HIPC(hipMalloc(&d_raw, rb));
+    hipStream_t st = ctx->lanes[0].stream;
+    HIPC(hipMemcpyAsync(d_raw, dist_raw.data(), rb, hipMemcpyHostToDevice, st));
+    const ncclResult_t r = ncclAllReduce(d_raw, d_raw, dist_raw.size(), ncclFloat64, ncclSum, ctx->comm, st);
+    hipError_t e = hipMemcpyAsync(dist_raw.data(), d_raw, rb, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d_raw);
+    if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    HIPC(e);
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+      if (!ctx->probs[pi].dist) continue;
+      for (int ti = 0; ti < n_t; ++ti)
+        finish_obs(ctx->probs[pi], dist_raw.data() + (pi * (size_t)n_t + ti) * 7,
+                   obs_out + pi * DSE_N_OBS * (size_t)n_t + ti, (size_t)n_t);
+    }
   }
   ctx->last_q = (n_t - 1) & 1;
   ctx->evolved = true;
@@ -929,10 +1197,16 @@ int dse_get_state(dse_ctx* ctx, int problem, double* psi_out) {
   if (!psi_out) return fail(ctx, DSE_ERR_ARG, "null state");
   if (!ctx->evolved) return fail(ctx, DSE_ERR_STATE, "no evolved state (call dse_evolve first)");
   HIPC(hipSetDevice(ctx->device));
-  HostProblem& P = ctx->probs[problem];
+  int first = 0, count = 1;
+  int rc = hook_members(ctx, problem, &first, &count);
+  if (rc) return rc;
   const int bsel = ctx->last_q ? 2 : 0;
-  const size_t bytes = (size_t(1) << P.n) * sizeof(double2);
-  HIPC(hipMemcpy(psi_out, P.buf[bsel], bytes, hipMemcpyDeviceToHost));
+  double2* out = reinterpret_cast<double2*>(psi_out);
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    const size_t amps = size_t(1) << P.n_local;
+    HIPC(hipMemcpy(out + i * amps, P.buf[bsel], amps * sizeof(double2), hipMemcpyDeviceToHost));
+  }
   return DSE_OK;
 }
 

@@ -32,6 +32,7 @@ class Engine:
         self._h = C.c_void_p(h)
         self.device = device
         self.problems: list[Problem] = []
+        self._dims: list[int] = []       # state size the hooks of each problem id take
         if tile_bits is not None:
             self.set_option("tile_bits", tile_bits)
         self.set_option("time_kernels", 1.0 if time_kernels else 0.0)
@@ -66,38 +67,73 @@ class Engine:
         self._check(self._L.dse_set_option(self._h, key.encode(), float(value)))
 
     # -- problems --
-    def add(self, prob: Problem) -> int:
+    @staticmethod
+    def _tables(prob: Problem):
         n = prob.n_qubits
-        field = np.ascontiguousarray(prob.field, dtype=np.float64)
-        zz = np.ascontiguousarray(prob.zz, dtype=np.float64).reshape(n * n)
-        pair = np.ascontiguousarray(prob.pair, dtype=np.float64).reshape(n * n)
-        flip = np.ascontiguousarray(prob.flip, dtype=np.float64).reshape(4 * n)
+        return (np.ascontiguousarray(prob.field, dtype=np.float64),
+                np.ascontiguousarray(prob.zz, dtype=np.float64).reshape(n * n),
+                np.ascontiguousarray(prob.pair, dtype=np.float64).reshape(n * n),
+                np.ascontiguousarray(prob.flip, dtype=np.float64).reshape(4 * n))
+
+    def add(self, prob: Problem) -> int:
+        tabs = self._tables(prob)
         pid = self._check(self._L.dse_add_problem(
-            self._h, n, _lib.ptr(field), _lib.ptr(zz), _lib.ptr(pair), _lib.ptr(flip),
+            self._h, prob.n_qubits, *[_lib.ptr(a) for a in tabs],
             float(prob.shift), int(prob.psi0_index), int(prob.sea_mask), int(prob.rare_bit),
             float(prob.rare_z_const)))
         self.problems.append(prob)
+        self._dims.append(1 << prob.n_qubits)
         return pid
+
+    def add_sharded(self, prob: Problem, shard_bits: int, rank: int = -1) -> int:
+        """A register partitioned by its top ``shard_bits`` qubits (include/dse.h): all shards
+        on this device (rank -1, returns shard 0's id; its hooks take whole-register states) or
+        this process's shard ``rank`` of a register spread over processes (after dist_init)."""
+        tabs = self._tables(prob)
+        pid = self._check(self._L.dse_add_problem_sharded(
+            self._h, prob.n_qubits, *[_lib.ptr(a) for a in tabs],
+            float(prob.shift), int(prob.psi0_index), int(prob.sea_mask), int(prob.rare_bit),
+            float(prob.rare_z_const), int(shard_bits), int(rank)))
+        n_members = 1 if rank >= 0 else (1 << shard_bits)
+        for i in range(n_members):
+            self.problems.append(prob)
+            self._dims.append((1 << prob.n_qubits) if (rank < 0 and i == 0)
+                              else int(self._L.dse_problem_dim(self._h, pid + i)))
+        return pid
+
+    @staticmethod
+    def dist_unique_id() -> bytes:
+        buf = C.create_string_buffer(_lib.DSE_DIST_ID_BYTES)
+        if _lib.lib().dse_dist_unique_id(buf) != 0:
+            raise RuntimeError("dse_dist_unique_id (ncclGetUniqueId) failed")
+        return buf.raw
+
+    def dist_init(self, rank: int, world: int, uid: bytes) -> None:
+        """Join the RCCL communicator of a register partitioned over ``world`` processes."""
+        if len(uid) != _lib.DSE_DIST_ID_BYTES:
+            raise ValueError("unique id must have DSE_DIST_ID_BYTES bytes")
+        self._check(self._L.dse_dist_init(self._h, int(rank), int(world), uid))
 
     def clear(self) -> None:
         self._check(self._L.dse_clear(self._h))
         self.problems = []
+        self._dims = []
 
     # -- hot path --
     def apply_h(self, pid: int, psi: np.ndarray) -> np.ndarray:
-        n = self.problems[pid].n_qubits
+        dim = self._dims[pid]
         x = np.ascontiguousarray(psi, dtype=np.complex128)
-        if x.shape != (1 << n,):
-            raise ValueError(f"state must have shape ({1 << n},)")
+        if x.shape != (dim,):
+            raise ValueError(f"state must have shape ({dim},)")
         out = np.empty_like(x)
         self._check(self._L.dse_apply_h(self._h, pid, _lib.ptr(x), _lib.ptr(out)))
         return out
 
     def observables(self, pid: int, psi: np.ndarray) -> np.ndarray:
-        n = self.problems[pid].n_qubits
+        dim = self._dims[pid]
         x = np.ascontiguousarray(psi, dtype=np.complex128)
-        if x.shape != (1 << n,):
-            raise ValueError(f"state must have shape ({1 << n},)")
+        if x.shape != (dim,):
+            raise ValueError(f"state must have shape ({dim},)")
         out = np.empty(7)
         self._check(self._L.dse_observables(self._h, pid, _lib.ptr(x), _lib.ptr(out)))
         return out
@@ -112,8 +148,7 @@ class Engine:
         return out, st.as_dict()
 
     def state(self, pid: int) -> np.ndarray:
-        n = self.problems[pid].n_qubits
-        out = np.empty(1 << n, dtype=np.complex128)
+        out = np.empty(self._dims[pid], dtype=np.complex128)
         self._check(self._L.dse_get_state(self._h, pid, _lib.ptr(out)))
         return out
 

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Config 5: one register partitioned over GPUs.
+
+    torchrun --nnodes 1 --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_partitioned.py
+    python tools/bench_partitioned.py --loopback 8        # all 8 shards on one GPU (test mode)
+
+Rank r holds shard r of the N = n_sea + 1 qubit center_on register (top log2(world) qubits
+global, the rare spin among them); every Chebyshev term exchanges whole shards with the partner
+ranks the terms couple (RCCL send/recv, include/dse.h).  Rank 0 prints one JSON line: ms per H
+application, exchanged bytes per H application and rank, the observables at t_final.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from quantumsimulations_amd import problem as pb  # noqa: E402
+from quantumsimulations_amd.engine import Engine  # noqa: E402
+from quantumsimulations_amd.partitioned import (join, shard_bits_for,  # noqa: E402
+                                                simulate_rare_partitioned)
+from quantumsimulations_amd.sweep import sweep_point_params  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-sea", type=int, default=29)
+    ap.add_argument("--t-final", type=float, default=1e-5)
+    ap.add_argument("--steps", type=int, default=11)
+    ap.add_argument("--delta", type=float, default=50e3)
+    ap.add_argument("--loopback", type=int, default=0, help="all shards on one GPU (2, 4 or 8)")
+    a = ap.parse_args()
+    p = sweep_point_params(a.n_sea, a.delta, "center_on", a.t_final, a.steps)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    prob = pb.build_problem(p)
+    if a.loopback:
+        bits = shard_bits_for(a.loopback)
+        with Engine(0) as eng:
+            pid = eng.add_sharded(prob, bits)
+            t0 = time.perf_counter()
+            obs, st = eng.evolve(np.linspace(0.0, a.t_final, a.steps))
+            wall = time.perf_counter() - t0
+        obs_d = {k: float(obs[pid, j, -1]) for j, k in enumerate(pb.OBS_NAMES)}
+        shards, mode = a.loopback, "loopback (all shards on one GPU)"
+        st = dict(st, h_applications=st["h_applications"] / shards)   # counted once per shard
+    else:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")       # bootstrap only; the data path is RCCL in libdse
+        with Engine(local) as eng:
+            join(eng, rank, world, dist)
+            dist.barrier()
+            t0 = time.perf_counter()
+            _, obs, st = simulate_rare_partitioned(p, eng, rank, world)
+            wall = time.perf_counter() - t0
+            tt = torch.tensor([wall], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            wall = float(tt.item())
+        obs_d = {k: float(v[-1]) for k, v in obs.items()}
+        shards, mode = world, "RCCL send/recv between ranks"
+        dist.destroy_process_group()
+    n = prob.n_qubits
+    bits = shard_bits_for(shards)
+    n_masks = 0
+    hi = n - bits
+    for m in range(1, 1 << bits):          # partner masks the terms need (as libdse computes)
+        gbits = [hi + i for i in range(bits) if (m >> i) & 1]
+        if len(gbits) == 1:
+            b = gbits[0]
+            n_masks += int(np.any(prob.flip[b] != 0) or np.any(prob.pair[:, b] != 0)
+                           or np.any(prob.pair[b, :] != 0) or bool((prob.sea_mask >> b) & 1)
+                           or b == prob.rare_bit)
+        elif len(gbits) == 2:
+            n_masks += int(prob.pair[min(gbits), max(gbits)] != 0)
+    shard_bytes = (1 << (n - bits)) * 16
+    if rank == 0:
+        print(json.dumps({
+            "config": f"config 5: N={n} center_on delta={a.delta:g} Hz, t_final={a.t_final}, "
+                      f"{a.steps} outputs, {shards} shards ({mode})",
+            "wall_s": wall, "h_applications": st["h_applications"],
+            "ms_per_h_application": wall / max(st["h_applications"], 1) * 1e3,
+            "shard_GiB": shard_bytes / 2**30, "partner_masks": n_masks,
+            "exchange_bytes_per_h_per_rank": n_masks * shard_bytes,
+            "obs_t_final": obs_d,
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
