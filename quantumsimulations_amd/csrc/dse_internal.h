@@ -106,7 +106,8 @@ hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items,
 hipError_t set_ablate(int mask);
 hipError_t set_ablate_interval(int mask);
 bool interval_supported(int L);
-hipError_t launch_interval(int L, const DevProb* probs, const int2* items, int n_items, int q,
+// imag: every drive coefficient of the launched problems is purely imaginary (HostProblem::imag)
+hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items, int q,
                            int set, int* flags, int* err, hipStream_t st);
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
                       double* partial, hipStream_t st);

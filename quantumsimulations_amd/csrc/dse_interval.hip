@@ -2,24 +2,37 @@
 //
 // One launch propagates one output interval [t_m, t_{m+1}] of every problem whose register fits
 // one or two LDS tiles (n <= L + 1; the N = 14 sweep: center_off has n = 13, center_on and
-// shell_off n = 14).  Each workgroup owns one tile for all K terms of the interval:
-//   LDS        w_{k-1} (the tile being multiplied; 128 KiB at L = 13)
-//   registers  w_{k-2} (16 amplitudes per thread) and the new w_k
-//   global     acc (accumulated every third term, L2-resident) and, for 2-tile problems, the
-//              cross-tile contribution u published to the partner workgroup each term.
-// This replaces K launches of k_step_rb (each reloading the tile from HBM and writing w_k back)
-// by one launch with no per-term HBM traffic for the state.
+// shell_off n = 14).  Each workgroup owns one tile for all K Chebyshev terms of the interval:
+//   LDS        w_{k-1}, the tile being multiplied (128 KiB at L = 13)
+//   registers  w_{k-2} (prev) and the new w_k (out), 16 amplitudes per thread each
+//   global     acc (read-modify-write every third term, L2-resident) and, for 2-tile problems,
+//              the cross-tile operand exchanged with the partner workgroup every term.
 //
-// Cross-tile hand-off (2-tile problems, tiles A/B differ in the top bit L):
-//   u_{A->B}(x) = flip_L(b_B) w_A(x) + sum_{j<L} g_{j,L} [x_j == b_B] w_A(x ^ e_j)
-// is A's contribution to B's H application of the same term.  A computes it from its LDS tile
-// at the start of the term and writes it (real parts, then imaginary parts) with 8-byte
-// agent-scope (sc1) stores into a two-slot buffer; after its own tile terms it waits for those
-// stores (s_waitcnt vmcnt(0)), barriers, and publishes the term index with an sc1 flag store.
-// B polls the flag with sc1 loads (one lane, s_sleep, bounded), barriers and reads u with sc1
-// loads (MI355X_MICROARCH.md "Valid forms", row 1: one workgroup per CU).
-// Slots alternate with the term parity; a slot is rewritten only after the partner has published
-// the next term, i.e. after it finished reading the slot.
+// Thread t owns the amplitudes x = r * NT + t, r = 0..15 (the four top tile bits are register
+// bits).  One H application is
+//   phase 1  diagonal, drives and pairs among register bits      (own amplitudes, registers)
+//   phase 2  one LDS sweep per thread bit j: the partner thread t ^ e_j's amplitudes serve the
+//            drive flip of j and the pairs (j, register bit i)
+//   phase 3  pairs between two thread bits (partner t ^ e_i ^ e_j, rows with x_i == x_j)
+//   phase 4  the partner tile's contribution (2-tile problems)
+//   phase 5  w_k = 2 (H - beta) w_{k-1} / alpha - w_{k-2}; acc += c0 w_{k-2} + c1 w_{k-1} + c2 w_k
+//            every third term; w_k -> LDS
+// Partner reads go through registers in halves of 8 amplitudes (split on register bit 3) so the
+// kernel stays inside the 256-VGPR budget of 2 waves per SIMD without spilling.  Term tables are
+// read through the constant address space (scalar loads into SGPRs).
+//
+// Cross-tile hand-off (2-tile problems; tiles A/B differ in the top bit L).  What B needs from A
+// for term k is u_{A->B}(x) = flip_L(b_B) w_A(x) + sum_{j<L} g_{j,L} [x_j == b_B] w_A(x ^ e_j):
+//   * flip-only crossing (center geometry: the top bit is the rare spin, coupled by ZZ only):
+//     B applies the flip coefficient itself, so A hands over w_{k-1} raw.  A stores w_k with
+//     16-byte sc1 stores at the end of term k (w_0 is A's psi tile, readable as is);
+//   * crossing pairs (shell geometry): A computes u in a pre-pass at the start of the term.
+// Either way the stores drain under phase 1, then the tile publishes the term index with an sc1
+// flag store (after s_waitcnt vmcnt(0) and a barrier); the partner polls the flag with sc1 loads
+// (one lane, s_sleep, bounded), barriers and reads the operand with sc1 loads after phase 3
+// (MI355X_MICROARCH.md "Valid forms", row 1: one workgroup per CU).  Two slots alternate with the
+// term parity; a slot is rewritten only after the partner published the following term, i.e.
+// after it finished reading the slot.
 #include "dse_device.h"
 
 namespace dse {
@@ -34,16 +47,58 @@ hipError_t set_ablate_interval(int mask) {
 namespace {
 
 typedef __attribute__((address_space(1))) int gint;
+// constant address space: uniform loads become scalar loads (SGPRs, scalar cache)
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ cptr<T> cst(const T* p) {
+  return (cptr<T>)p;
+}
 
 constexpr int kSpinLimit = 1 << 22;  // ~0.3 s of polling before the hand-off is declared failed
 
+// out += c * s for a drive coefficient c = cr + i ci; IMAG: cr == 0 (drive phase pi/2)
+template <bool IMAG>
+__device__ __forceinline__ double2 dmad(double2 acc, double cr, double ci, double2 s) {
+  if (IMAG) {
+    acc.x = fma(-ci, s.y, acc.x);
+    acc.y = fma(ci, s.x, acc.y);
+    return acc;
+  }
+  return cmad(acc, cr, ci, s);
+}
+
+__device__ __forceinline__ void rmad(double2& acc, double g, double2 s) {
+  acc.x = fma(g, s.x, acc.x);
+  acc.y = fma(g, s.y, acc.y);
+}
+
 template <int L>
+struct IvShared {
+  double2 w[RB<L>::T];  // the tile of w_{k-1}
+  double c[L + 1];      // F_i(h) (i < L) and C(h) of the tile
+  double zz[L * L];     // in-tile zz couplings (upper triangle)
+  double zr[kRegAmps];  // register-bit ZZ part of the diagonal per r
+};
+
+// Sweep pairs (thread bit j, register bit i < 3) of half hh for a wave-uniform bit value BJ.
+template <int BJ, int NH>
+__device__ __forceinline__ void sweep_pairs_uniform(const double* g, const double2* pv, double2* out_h) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int rr = 0; rr < NH; ++rr)
+      if (((rr >> i) & 1) == BJ) rmad(out_h[rr], g[i], pv[rr ^ (1 << i)]);
+}
+
+template <int L, bool IMAG>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
            int* __restrict__ flags, int* __restrict__ err) {
-  constexpr int NT = RB<L>::NT, R = kRegAmps;
-  constexpr size_t T = size_t(1) << L;
-  __shared__ RBShared<L> S;
+  constexpr int NT = RB<L>::NT, R = kRegAmps, TB = RB<L>::TB, NH = R / 2;
+  constexpr int LANE_BITS = TB < 6 ? TB : 6;
+  constexpr uint32_t T = 1u << L;
+  __shared__ IvShared<L> S;
   __shared__ int s_fail;
 
   const int2 it = items[blockIdx.x];
@@ -51,12 +106,14 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const uint32_t h = (uint32_t)it.y;
   const int tid = threadIdx.x;
   const bool pair = (P.n == L + 1);
+  const bool xgen = pair && P.n_pairs_hi > 0;  // pairs cross the tile boundary: u pre-pass
+  const bool xraw = pair && !xgen;             // only the top-bit drive crosses: raw w exchange
   const int K = P.degree;
   const double s1 = P.s1;
+  const uint32_t b_me = h & 1u, b_pa = b_me ^ 1u;  // top-bit values of this / the partner tile
 
-  // exchange slots (AoS double2, sc1): term parity 0 -> psi region (free once w_0 is in LDS),
-  // 1 -> scratch buffer
-  constexpr uint32_t TBYTES = uint32_t(T) * 16u;
+  // slots (AoS double2, sc1): term parity 0 -> psi region (free once w_0 is in LDS), 1 -> scratch
+  constexpr uint32_t TBYTES = T * 16u;
   const __amdgpu_buffer_rsrc_t slot_me[2] = {tile_rsrc(P.buf[q ? 2 : 0] + (h << L), TBYTES),
                                              tile_rsrc(P.buf[1] + (h << L), TBYTES)};
   const __amdgpu_buffer_rsrc_t slot_pa[2] = {tile_rsrc(P.buf[q ? 2 : 0] + ((h ^ 1u) << L), TBYTES),
@@ -65,97 +122,286 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const uint32_t voff = (uint32_t)tid * 16u;
   gint* flag_me = (gint*)flags + 2 * it.x + h;
   const gint* flag_pa = (const gint*)flags + 2 * it.x + (h ^ 1u);
-  const uint32_t b_pa = (h ^ 1u) & 1u;  // top-bit value of the partner tile
 
-  // diagnostics only (0 in production): 64 skip the u publication, 128 skip the partner wait and
-  // read, 256 skip the acc updates, 512 skip the own-tile H terms
+  // term tables (scalar loads)
+  const cptr<DSweep> csw = cst(P.sweeps);
+  const cptr<DPair> ctt = cst(P.pairs_tt);
+  const cptr<DPair> cph = cst(P.pairs_hi);
+  const cptr<DFlip> cfh = cst(P.flips_hi);
+  const cptr<CoefK> ccoef = cst(P.coef + set * P.kcap1);
+  const int n_tt = P.n_pairs_tt;
+  // the top-bit drive (cross flip) for this tile's output bit value (raw exchange)
+  double xr = 0.0, xi = 0.0;
+  if (pair && P.n_flips_hi > 0) {
+    xr = b_me ? cfh[0].re1 : cfh[0].re0;
+    xi = b_me ? cfh[0].im1 : cfh[0].im0;
+  }
+
+  // diagnostics only (0 in production): 64 skip the hand-off stores and flag, 128 skip the
+  // partner wait and read, 256 skip the acc updates, 512 skip the tile terms
   const int ab = g_dse_ablate_iv;
+
+  // ---- setup: tables, w_0 tile -> LDS, per-thread diagonal ----
   if (tid == 0) s_fail = 0;
-  rb_stage_tables<L>(S, P, h, P.beta, tid);
+  {
+    const gdbl* zz = gptr(P.zz);
+    const int n = P.n;
+    for (int e = tid; e < L * L; e += NT) {
+      const int i = e / L, j = e % L;
+      S.zz[e] = (j > i) ? zz[i * n + j] : 0.0;
+    }
+    tile_diag_coeffs<L>(P, h, P.beta, S.c, tid);
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) S.w[r * NT + tid] = bld(slot_me[0], voff, (uint32_t)(r * NT * 16));
   __syncthreads();
-  rb_register_zz<L>(S, tid);
-  const ThreadDiag td = rb_thread_diag<L>(S, tid);
+  if (tid < kRegAmps) {
+    double v = 0.0;
+    for (int a = 0; a < kRegBits; ++a)
+      for (int b = a + 1; b < kRegBits; ++b)
+        v += S.zz[(TB + a) * L + TB + b] * ((0.5 - ((tid >> a) & 1)) * (0.5 - ((tid >> b) & 1)));
+    S.zr[tid] = v;
+  }
+  // per-thread diagonal: D(r) = zt + sum_i hr[i] s_i(r) + zr[r]
+  double zt = S.c[L];
+  double hr[kRegBits];
+#pragma unroll
+  for (int i = 0; i < kRegBits; ++i) hr[i] = S.c[TB + i];
+#pragma unroll 1
+  for (int j = 0; j < TB; ++j) {
+    const double sj = 0.5 - (double)((tid >> j) & 1);
+    double a = S.c[j];
+#pragma unroll 1
+    for (int i = j + 1; i < TB; ++i) a += S.zz[j * L + i] * (0.5 - (double)((tid >> i) & 1));
+    zt += a * sj;
+#pragma unroll
+    for (int i = 0; i < kRegBits; ++i) hr[i] += S.zz[j * L + TB + i] * sj;
+  }
+  // register-bit cross pairs (register bit i, top bit) for the u pre-pass
+  double xg_reg[kRegBits] = {0.0, 0.0, 0.0, 0.0};
+  if (xgen)
+    for (int p = 0; p < P.n_pairs_hi; ++p) {
+      const uint32_t m = cph[p].mask_lo;
+      if (m >= (1u << TB)) {
+        const int i = __builtin_ctz(m) - TB;
+#pragma unroll
+        for (int c = 0; c < kRegBits; ++c)
+          if (c == i) xg_reg[c] = cph[p].g;
+      }
+    }
   __syncthreads();
 
   double2 prev[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) prev[r] = make_double2(0.0, 0.0);
+
   for (int k = 1; k <= K; ++k) {
-    // ---- u(w_{k-1}) for the partner: computed and stored (16-byte sc1 stores) before the
-    // tile terms, published after them so the write-through drains under the compute ----
-    const __amdgpu_buffer_rsrc_t dst = slot_me[(k - 1) & 1];
-    if (pair && !(ab & 64)) {
+    // ---- phase 0 (crossing pairs): u(w_{k-1}) for the partner -> slot (k-1)&1, sc1 ----
+    if (xgen && !(ab & 64)) {
       double2 u[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) u[r] = make_double2(0.0, 0.0);
-      // cross flip of the top bit: coefficient for the partner's output bit value
-      for (int f = 0; f < P.n_flips_hi; ++f) {
-        const DFlip F = S.fh[f];
-        const double cr = b_pa ? F.re1 : F.re0, ci = b_pa ? F.im1 : F.im0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) u[r] = cmad(u[r], cr, ci, S.w[r * NT + tid]);
-      }
-      // cross pairs (j, top): applies iff x_j == b_pa; source w_A(x ^ e_j)
-      for (int p = 0; p < P.n_pairs_hi; ++p) {
-        const DPair Q = S.ph[p];
-        const uint32_t m = Q.mask_lo;
+      for (int hh = 0; hh < 2; ++hh) {
+        double2 ow[NH];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const uint32_t x = (uint32_t)(r * NT + tid);
-          const double g = (((x & m) != 0u) == (b_pa != 0u)) ? Q.g : 0.0;
-          const double2 sv = S.w[x ^ m];
-          u[r].x = fma(g, sv.x, u[r].x);
-          u[r].y = fma(g, sv.y, u[r].y);
+        for (int rr = 0; rr < NH; ++rr) ow[rr] = S.w[(hh * NH + rr) * NT + tid];
+        for (int f = 0; f < P.n_flips_hi; ++f) {  // top-bit drive at the partner's bit value
+          const double cr = b_pa ? cfh[f].re1 : cfh[f].re0, ci = b_pa ? cfh[f].im1 : cfh[f].im0;
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) u[hh * NH + rr] = cmad(u[hh * NH + rr], cr, ci, ow[rr]);
+        }
+        // (register bit i, top): output rows with r_i == b_pa, source r ^ e_i
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) {
+            const double g = (((rr >> i) & 1u) == b_pa) ? xg_reg[i] : 0.0;
+            rmad(u[hh * NH + rr], g, ow[rr ^ (1 << i)]);
+          }
+        {
+          const double g = ((uint32_t)(1 - hh) == b_pa) ? xg_reg[3] : 0.0;
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) rmad(u[(1 - hh) * NH + rr], g, ow[rr]);
         }
       }
+      // (thread bit j, top): applies iff t_j == b_pa, source t ^ e_j
+      for (int p = 0; p < P.n_pairs_hi; ++p) {
+        const uint32_t m = cph[p].mask_lo;
+        if (m >= (1u << TB)) continue;
+        if ((((uint32_t)tid & m) != 0u) != (b_pa != 0u)) continue;
+        const double g = cph[p].g;
+        const int pt = tid ^ (int)m;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          double2 pv[NH];
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) rmad(u[hh * NH + rr], g, pv[rr]);
+        }
+      }
+      const __amdgpu_buffer_rsrc_t dst = slot_me[(k - 1) & 1];
 #pragma unroll
       for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), u[r]);
     }
 
-    // ---- out = (H - beta) w_{k-1}: own-tile terms ----
+    // ---- phase 1: diagonal and register-bit terms ----
     double2 out[R];
-    if (ab & 512) {
+    {
+      double2 own[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) out[r] = S.w[r * NT + tid];
-    } else {
-      rb_apply_tile_a<L>(S, P, tid, td, 0, out);
-      rb_apply_tile_b<L>(S, P, tid, 0, out);
+      for (int r = 0; r < R; ++r) own[r] = S.w[r * NT + tid];
+      if (ab & 512) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) out[r] = own[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          double d = zt + S.zr[r];
+#pragma unroll
+          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * hr[i];
+          out[r].x = d * own[r].x;
+          out[r].y = d * own[r].y;
+        }
+        if (P.rflip_mask) {
+#pragma unroll
+          for (int i = 0; i < kRegBits; ++i) {
+            if (!((P.rflip_mask >> i) & 1)) continue;
+            const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const bool v = (r >> i) & 1;
+              out[r] = dmad<IMAG>(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
+            }
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < kRegBits; ++a)
+#pragma unroll
+          for (int b = a + 1; b < kRegBits; ++b) {
+            const double g = P.rr_g[rr_index(a, b)];
+            if (g == 0.0) continue;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
+              rmad(out[r], g, own[r ^ ((1 << a) | (1 << b))]);
+            }
+          }
+      }
     }
 
-    // ---- publish, then add the partner's contribution u(w_{k-1}) ----
-    if (pair && !(ab & 64)) {
+    // ---- publish: the hand-off stores of this term have drained under phase 1 ----
+    if (pair && !(ab & 64) && (xgen || k > 1)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (pair && !(ab & 128)) {
-      if (tid == 0 && !(ab & 64)) {
-        int spins = 0;
-        while (__hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > kSpinLimit) {
-            s_fail = 1;
-            atomicExch(err, 1);
-            break;
+
+    if (!(ab & 512)) {
+      // ---- phase 2: thread-bit sweeps ----
+#pragma unroll 1
+      for (int j = 0; j < TB; ++j) {
+        const int has_flip = csw[j].has_flip, has_pair = csw[j].has_pair;
+        if (!(has_flip | has_pair)) continue;
+        const int bj = (tid >> j) & 1;
+        const int pt = tid ^ (1 << j);
+        const double cr = bj ? csw[j].re1 : csw[j].re0, ci = bj ? csw[j].im1 : csw[j].im0;
+        double g[kRegBits];
+#pragma unroll
+        for (int i = 0; i < kRegBits; ++i) g[i] = csw[j].g[i];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          double2 pv[NH];
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+          double2* oh = out + hh * NH;
+          if (has_flip) {
+#pragma unroll
+            for (int rr = 0; rr < NH; ++rr) oh[rr] = dmad<IMAG>(oh[rr], cr, ci, pv[rr]);
+          }
+          if (has_pair) {
+            if (j >= LANE_BITS) {  // a wave-index bit: bj is uniform, touch only the rows it pairs
+              if (bj)
+                sweep_pairs_uniform<1, NH>(g, pv, oh);
+              else
+                sweep_pairs_uniform<0, NH>(g, pv, oh);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 3; ++i) {
+                const double g0 = bj ? 0.0 : g[i], g1 = bj ? g[i] : 0.0;  // iff r_i == bj
+#pragma unroll
+                for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ((rr >> i) & 1) ? g1 : g0, pv[rr ^ (1 << i)]);
+              }
+            }
+            // (j, register bit 3): rows of the other half, iff r_3 = 1 - hh == bj
+            const double g3 = (1 - hh == bj) ? g[3] : 0.0;
+            double2* oo = out + (1 - hh) * NH;
+#pragma unroll
+            for (int rr = 0; rr < NH; ++rr) rmad(oo[rr], g3, pv[rr]);
           }
         }
       }
-      __syncthreads();
-      const __amdgpu_buffer_rsrc_t src = slot_pa[(k - 1) & 1];
-      double2 uv[R];
+
+      // ---- phase 3: pairs between two thread bits ----
+#pragma unroll 1
+      for (int p = 0; p < n_tt; ++p) {
+        const uint32_t m = ctt[p].mask_lo;
+        if (par32((uint32_t)tid & m)) continue;  // rows with x_i == x_j
+        const double g = ctt[p].g;
+        const int pt = tid ^ (int)m;
 #pragma unroll
-      for (int r = 0; r < R; ++r) uv[r] = bld<kSc1>(src, voff, (uint32_t)(r * NT * 16));
+        for (int hh = 0; hh < 2; ++hh) {
+          double2 pv[NH];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        out[r].x += uv[r].x;
-        out[r].y += uv[r].y;
+          for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) rmad(out[hh * NH + rr], g, pv[rr]);
+        }
       }
     }
 
-    // ---- recurrence + accumulation (in place in out[], acc operands four registers at a time
-    // to bound the live registers) ----
-    const CoefK C = P.coef[set * P.kcap1 + k];
-    const bool upd = C.upd && !(ab & 256);
+    // ---- phase 4: the partner tile's contribution ----
+    if (pair && !(ab & 128)) {
+      __amdgpu_buffer_rsrc_t src = slot_pa[(k - 1) & 1];
+      const bool need_flag = xgen || k > 1;  // w_0 of the partner is its psi tile, already visible
+      if (need_flag) {
+        if (tid == 0 && !(ab & 64)) {
+          int spins = 0;
+          while (__hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > kSpinLimit) {
+              s_fail = 1;
+              atomicExch(err, 1);
+              break;
+            }
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        double2 uv[NH];
+#pragma unroll
+        for (int rr = 0; rr < NH; ++rr) uv[rr] = bld<kSc1>(src, voff, (uint32_t)((hh * NH + rr) * NT * 16));
+        if (xgen) {
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) {
+            out[hh * NH + rr].x += uv[rr].x;
+            out[hh * NH + rr].y += uv[rr].y;
+          }
+        } else {
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) out[hh * NH + rr] = dmad<IMAG>(out[hh * NH + rr], xr, xi, uv[rr]);
+        }
+      }
+    }
+
+    // ---- phase 5: recurrence + accumulation (acc operands four registers at a time) ----
+    const cptr<double> cc = (cptr<double>)(ccoef + k);  // c[0..2] as (re, im) pairs
+    const double2 c0 = make_double2(cc[0], cc[1]), c1 = make_double2(cc[2], cc[3]),
+                  c2 = make_double2(cc[4], cc[5]);
+    const bool upd = ccoef[k].upd && !(ab & 256);
 #pragma unroll
     for (int r0 = 0; r0 < R; r0 += 4) {
       double2 accv[4];
@@ -170,17 +416,17 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
           out[r].x *= s1;
           out[r].y *= s1;
           double2 a = make_double2(0.0, 0.0);
-          a = cmad(a, C.c[1].x, C.c[1].y, own);
-          a = cmad(a, C.c[2].x, C.c[2].y, out[r]);
+          a = cmad(a, c1.x, c1.y, own);
+          a = cmad(a, c2.x, c2.y, out[r]);
           bst(acc_t, voff, (uint32_t)(r * NT * 16), a);
         } else {
           out[r].x = fma(2.0 * s1, out[r].x, -prev[r].x);
           out[r].y = fma(2.0 * s1, out[r].y, -prev[r].y);
           if (upd) {
             double2 a = accv[r - r0];
-            a = cmad(a, C.c[0].x, C.c[0].y, prev[r]);
-            a = cmad(a, C.c[1].x, C.c[1].y, own);
-            a = cmad(a, C.c[2].x, C.c[2].y, out[r]);
+            a = cmad(a, c0.x, c0.y, prev[r]);
+            a = cmad(a, c1.x, c1.y, own);
+            a = cmad(a, c2.x, c2.y, out[r]);
             bst(acc_t, voff, (uint32_t)(r * NT * 16), a);
           }
         }
@@ -190,6 +436,11 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
     __syncthreads();  // every read of w_{k-1} in LDS is done
 #pragma unroll
     for (int r = 0; r < R; ++r) S.w[r * NT + tid] = out[r];
+    if (xraw && k < K && !(ab & 64)) {  // w_k for the partner's term k + 1
+      const __amdgpu_buffer_rsrc_t dst = slot_me[k & 1];
+#pragma unroll
+      for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), out[r]);
+    }
     __syncthreads();
     if (s_fail) break;  // uniform: a hand-off timed out (error reported to the host)
   }
@@ -199,14 +450,18 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 
 bool interval_supported(int L) { return L >= kRegBlockMinTile && L <= kMaxTile; }
 
-hipError_t launch_interval(int L, const DevProb* probs, const int2* items, int n_items, int q,
-                           int set, int* flags, int* err, hipStream_t st) {
+hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items,
+                           int q, int set, int* flags, int* err, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   switch (L) {
-#define X(l)                                                                                  \
-  case l:                                                                                     \
-    hipLaunchKernelGGL((k_interval<l>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs, items, q, \
-                       set, flags, err);                                                      \
+#define X(l)                                                                                     \
+  case l:                                                                                        \
+    if (imag)                                                                                    \
+      hipLaunchKernelGGL((k_interval<l, true>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs,  \
+                         items, q, set, flags, err);                                             \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_interval<l, false>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs, \
+                         items, q, set, flags, err);                                             \
     return hipGetLastError();
     X(10) X(11) X(12) X(13)
 #undef X

@@ -58,6 +58,7 @@ struct HostProblem {
   bool dist = false;         // shard of a register partitioned over processes (RCCL exchange)
   uint32_t xmasks = 0;       // bit m set: terms or observables read shard rank ^ m
   double2* rbuf_own[kMaxShards] = {};  // dist: receive buffers of the exchange, per mask
+  bool imag = false;         // every drive coefficient purely imaginary (drive phase pi/2)
 };
 
 // One stream's share of the problems, grouped by tile size.
@@ -88,6 +89,7 @@ struct dse_ctx {
   std::vector<DevProb> h_desc;
   std::vector<Lane> lanes;
   int2* d_items = nullptr;          // all items, lane-major, degree-sorted inside each group
+  int2* d_items_iv = nullptr;       // the same, 2-tile groups reordered for the interval kernel
   std::vector<int64_t> item_pos;    // first item position of every problem (evolve layout)
   int64_t total_items = 0;
   double* d_partial = nullptr;
@@ -141,6 +143,7 @@ void free_device(dse_ctx* ctx) {
   }
   if (ctx->d_probs) (void)hipFree(ctx->d_probs), ctx->d_probs = nullptr;
   if (ctx->d_items) (void)hipFree(ctx->d_items), ctx->d_items = nullptr;
+  if (ctx->d_items_iv) (void)hipFree(ctx->d_items_iv), ctx->d_items_iv = nullptr;
   if (ctx->d_partial) (void)hipFree(ctx->d_partial), ctx->d_partial = nullptr;
   for (auto& kv : ctx->zzlo_tables) (void)hipFree(kv.second);
   if (ctx->d_flags) (void)hipFree(ctx->d_flags), ctx->d_flags = nullptr;
@@ -224,9 +227,20 @@ int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
         sweeps[i].has_pair = 1;
       }
     }
+  p.imag = true;
   for (int b = 0; b < n; ++b) {
-    const double* f = &p.flip[4 * b];
+    // A real part below 1e-15 of the coefficient's modulus is the rounding residue of cos(pi/2)
+    // (the reference's drive phase, dipolar_ensemble_with_rare.py:516-530): it is dropped, so
+    // drives at phase pi/2 take the imaginary-coefficient kernels (2 FMAs per amplitude, not 4).
+    // The dropped entry is 1e-16 of its row's drive term, below the rounding of H itself.
+    double f[4];
+    for (int c = 0; c < 4; c += 2) {
+      f[c] = p.flip[4 * b + c];
+      f[c + 1] = p.flip[4 * b + c + 1];
+      if (std::fabs(f[c]) <= 1e-15 * std::hypot(f[c], f[c + 1])) f[c] = 0.0;
+    }
     if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
+    if (f[0] != 0.0 || f[2] != 0.0) p.imag = false;
     const uint64_t m = uint64_t(1) << b;
     DFlip q;
     q.mask_lo = (uint32_t)(m & lo_mask);
@@ -375,7 +389,8 @@ int prepare(dse_ctx* ctx) {
     }
   }
   if (hipMalloc(&ctx->d_probs, dp.size() * sizeof(DevProb)) != hipSuccess ||
-      hipMalloc(&ctx->d_items, total * sizeof(int2)) != hipSuccess) {
+      hipMalloc(&ctx->d_items, total * sizeof(int2)) != hipSuccess ||
+      hipMalloc(&ctx->d_items_iv, total * sizeof(int2)) != hipSuccess) {
     free_device(ctx);
     return fail(ctx, DSE_ERR_OOM, "device allocation of descriptors failed");
   }
@@ -996,6 +1011,31 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     max_deg = std::max(max_deg, ln.max_deg);
   }
   HIPC(hipMemcpy(ctx->d_items, items.data(), items.size() * sizeof(int2), hipMemcpyHostToDevice));
+  bool imag_all = true;
+  for (auto& P : ctx->probs) imag_all = imag_all && P.imag;
+  if (persistent) {
+    // Interval-kernel order of 2-tile groups: the two tiles of a problem exchange data every
+    // term, so place them 8 blocks apart -- blocks b and b + 8 land on one XCD under the
+    // observed round-robin dispatch and then hand off through that XCD's L2 (speed only; the
+    // hand-off protocol does not depend on placement).  Chunks of one launch are multiples of 16.
+    std::vector<int2> iv = items;
+    const int64_t cap = std::max<int64_t>(2, (ctx->n_cu / 2) * 2);
+    for (auto& ln : ctx->lanes)
+      for (auto& g : ln.groups) {
+        if (g.tiles != 2) continue;
+        for (int64_t off = 0; off < g.count; off += cap) {
+          const int64_t cnt = std::min<int64_t>(cap, g.count - off);
+          for (int64_t b0 = 0; b0 < cnt; b0 += 16) {
+            const int64_t m = std::min<int64_t>(16, cnt - b0) / 2;  // problems in this block
+            for (int64_t i = 0; i < m; ++i) {
+              iv[g.off + off + b0 + i] = items[g.off + off + b0 + 2 * i];
+              iv[g.off + off + b0 + m + i] = items[g.off + off + b0 + 2 * i + 1];
+            }
+          }
+        }
+      }
+    HIPC(hipMemcpy(ctx->d_items_iv, iv.data(), iv.size() * sizeof(int2), hipMemcpyHostToDevice));
+  }
   if (persistent) {
     const size_t need = 2 * ctx->probs.size() + 1;
     if (ctx->flags_cap < need) {
@@ -1088,11 +1128,11 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
             if (timed) {
               const size_t i = ln.ev_used[pool]++;
               HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
-              HIPC(launch_interval(g.L, ctx->d_probs, ctx->d_items + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
+              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
               HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
               pool_bytes[li * 2 + pool].push_back(fl);
             } else {
-              HIPC(launch_interval(g.L, ctx->d_probs, ctx->d_items + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
+              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
             }
             launches += 1.0;
             amp_updates += am;

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Iteration pass: gpu parity tests, interval-kernel ablation probe, bench without the CPU leg.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python -u tools/probe_interval.py > gpurun_out/probe.jsonl 2> gpurun_out/probe.err && \
+timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
