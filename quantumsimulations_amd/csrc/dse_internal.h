@@ -19,6 +19,7 @@ constexpr int kRegBlockMinTile = 6 + kRegBits;    // tiles >= 2^10 (>= one wave)
 __host__ __device__ constexpr int rr_index(int a, int b) {
   return a * (2 * kRegBits - a - 1) / 2 + (b - a - 1);
 }
+constexpr int kXSlots = 4;                        // hand-off ring of the interval kernel
 constexpr int kMaxShardBits = 3;                  // partitioned registers: up to 8 shards
 constexpr int kMaxShards = 1 << kMaxShardBits;
 // bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index
@@ -92,6 +93,7 @@ struct DevProb {
   uint32_t h_base;        // rank << tbl (0 for an ordinary problem)
   int tbl;                // local tile-index bits: log2(tiles of this shard)
   double2* rbuf[kMaxShards][3];
+  double2* xslots;        // interval kernel, 2-tile problems: [2][kXSlots][2^L] hand-off slots
 };
 
 // Global tile hp of the role-`role` vector: local buffer or a partner shard's.

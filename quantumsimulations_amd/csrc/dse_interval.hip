@@ -30,9 +30,13 @@
 // Either way the stores drain under phase 1, then the tile publishes the term index with an sc1
 // flag store (after s_waitcnt vmcnt(0) and a barrier); the partner polls the flag with sc1 loads
 // (one lane, s_sleep, bounded), barriers and reads the operand with sc1 loads after phase 3
-// (MI355X_MICROARCH.md "Valid forms", row 1: one workgroup per CU).  Two slots alternate with the
-// term parity; a slot is rewritten only after the partner published the following term, i.e.
-// after it finished reading the slot.
+// (MI355X_MICROARCH.md "Valid forms", row 1: one workgroup per CU).  Slots form a ring of
+// kXSlots per tile; a slot is rewritten kXSlots terms later, and every term waits for the
+// partner's flag of that term, so the partner has long finished reading it.
+//
+// Register budget: this kernel must not spill VGPRs.  A build that spilled 12 VGPRs (stored once in
+// the prologue, reloaded every term) gave run-to-run differences of ~1e-9 on 2-tile problems;
+// tests/test_build.py checks the resource usage and tests/test_gpu_parity.py bitwise determinism.
 #include "dse_device.h"
 
 namespace dse {
@@ -79,6 +83,10 @@ struct IvShared {
   double c[L + 1];      // F_i(h) (i < L) and C(h) of the tile
   double zz[L * L];     // in-tile zz couplings (upper triangle)
   double zr[kRegAmps];  // register-bit ZZ part of the diagonal per r
+  // per-thread diagonal D(r) = td[0] + sum_i td[1 + i] s_i(r) + zr[r], kept here rather than in
+  // registers: the kernel is at the 256-VGPR limit and these are read once per term
+  double td[1 + kRegBits][RB<L>::NT];
+  double xg[kRegBits];  // cross pairs (register bit i, top bit) of the u pre-pass
 };
 
 // Sweep pairs (thread bit j, register bit i < 3) of half hh for a wave-uniform bit value BJ.
@@ -112,12 +120,14 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const double s1 = P.s1;
   const uint32_t b_me = h & 1u, b_pa = b_me ^ 1u;  // top-bit values of this / the partner tile
 
-  // slots (AoS double2, sc1): term parity 0 -> psi region (free once w_0 is in LDS), 1 -> scratch
+  // hand-off slots (AoS double2, sc1): a ring of kXSlots tile-sized regions per tile,
+  // P.xslots[(tile * kXSlots + (k - 1) % kXSlots) << L] carries the operand of term k.  The
+  // partner's w_0 is read from its psi tile.
   constexpr uint32_t TBYTES = T * 16u;
-  const __amdgpu_buffer_rsrc_t slot_me[2] = {tile_rsrc(P.buf[q ? 2 : 0] + (h << L), TBYTES),
-                                             tile_rsrc(P.buf[1] + (h << L), TBYTES)};
-  const __amdgpu_buffer_rsrc_t slot_pa[2] = {tile_rsrc(P.buf[q ? 2 : 0] + ((h ^ 1u) << L), TBYTES),
-                                             tile_rsrc(P.buf[1] + ((h ^ 1u) << L), TBYTES)};
+  const __amdgpu_buffer_rsrc_t psi_me = tile_rsrc(P.buf[q ? 2 : 0] + (h << L), TBYTES);
+  const __amdgpu_buffer_rsrc_t psi_pa = tile_rsrc(P.buf[q ? 2 : 0] + ((h ^ 1u) << L), TBYTES);
+  double2* const xs_me = P.xslots + ((size_t)h * kXSlots << L);
+  double2* const xs_pa = P.xslots + ((size_t)(h ^ 1u) * kXSlots << L);
   const __amdgpu_buffer_rsrc_t acc_t = tile_rsrc(P.buf[q ? 0 : 2] + (h << L), TBYTES);
   const uint32_t voff = (uint32_t)tid * 16u;
   gint* flag_me = (gint*)flags + 2 * it.x + h;
@@ -137,8 +147,9 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
     xi = b_me ? cfh[0].im1 : cfh[0].im0;
   }
 
-  // diagnostics only (0 in production): 64 skip the hand-off stores and flag, 128 skip the
-  // partner wait and read, 256 skip the acc updates, 512 skip the tile terms
+  // diagnostics only (0 in production): 1 skip the sweeps, 2 skip the thread-bit pairs, 4 skip
+  // the register-bit terms, 64 skip the hand-off stores and flag, 128 skip the partner wait and
+  // read, 256 skip the acc updates, 512 skip the tile terms
   const int ab = g_dse_ablate_iv;
 
   // ---- setup: tables, w_0 tile -> LDS, per-thread diagonal ----
@@ -153,7 +164,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
     tile_diag_coeffs<L>(P, h, P.beta, S.c, tid);
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) S.w[r * NT + tid] = bld(slot_me[0], voff, (uint32_t)(r * NT * 16));
+  for (int r = 0; r < R; ++r) S.w[r * NT + tid] = bld(psi_me, voff, (uint32_t)(r * NT * 16));
   __syncthreads();
   if (tid < kRegAmps) {
     double v = 0.0;
@@ -177,18 +188,17 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
     for (int i = 0; i < kRegBits; ++i) hr[i] += S.zz[j * L + TB + i] * sj;
   }
-  // register-bit cross pairs (register bit i, top bit) for the u pre-pass
-  double xg_reg[kRegBits] = {0.0, 0.0, 0.0, 0.0};
-  if (xgen)
-    for (int p = 0; p < P.n_pairs_hi; ++p) {
-      const uint32_t m = cph[p].mask_lo;
-      if (m >= (1u << TB)) {
-        const int i = __builtin_ctz(m) - TB;
+  S.td[0][tid] = zt;
 #pragma unroll
-        for (int c = 0; c < kRegBits; ++c)
-          if (c == i) xg_reg[c] = cph[p].g;
-      }
-    }
+  for (int i = 0; i < kRegBits; ++i) S.td[1 + i][tid] = hr[i];
+  // register-bit cross pairs (register bit i, top bit) for the u pre-pass
+  if (tid < kRegBits) {
+    double g = 0.0;
+    if (xgen)
+      for (int p = 0; p < P.n_pairs_hi; ++p)
+        if (cph[p].mask_lo == (1u << (TB + tid))) g = cph[p].g;
+    S.xg[tid] = g;
+  }
   __syncthreads();
 
   double2 prev[R];
@@ -216,11 +226,11 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int rr = 0; rr < NH; ++rr) {
-            const double g = (((rr >> i) & 1u) == b_pa) ? xg_reg[i] : 0.0;
+            const double g = (((rr >> i) & 1u) == b_pa) ? S.xg[i] : 0.0;
             rmad(u[hh * NH + rr], g, ow[rr ^ (1 << i)]);
           }
         {
-          const double g = ((uint32_t)(1 - hh) == b_pa) ? xg_reg[3] : 0.0;
+          const double g = ((uint32_t)(1 - hh) == b_pa) ? S.xg[3] : 0.0;
 #pragma unroll
           for (int rr = 0; rr < NH; ++rr) rmad(u[(1 - hh) * NH + rr], g, ow[rr]);
         }
@@ -241,7 +251,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
           for (int rr = 0; rr < NH; ++rr) rmad(u[hh * NH + rr], g, pv[rr]);
         }
       }
-      const __amdgpu_buffer_rsrc_t dst = slot_me[(k - 1) & 1];
+      const __amdgpu_buffer_rsrc_t dst = tile_rsrc(xs_me + ((size_t)((k - 1) % kXSlots) << L), TBYTES);
 #pragma unroll
       for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), u[r]);
     }
@@ -252,15 +262,15 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       double2 own[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) own[r] = S.w[r * NT + tid];
-      if (ab & 512) {
+      if (ab & (512 | 4)) {
 #pragma unroll
         for (int r = 0; r < R; ++r) out[r] = own[r];
       } else {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          double d = zt + S.zr[r];
+          double d = S.td[0][tid] + S.zr[r];
 #pragma unroll
-          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * hr[i];
+          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * S.td[1 + i][tid];
           out[r].x = d * own[r].x;
           out[r].y = d * own[r].y;
         }
@@ -295,13 +305,15 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
     if (pair && !(ab & 64) && (xgen || k > 1)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {
+        __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
 
     if (!(ab & 512)) {
       // ---- phase 2: thread-bit sweeps ----
 #pragma unroll 1
-      for (int j = 0; j < TB; ++j) {
+      for (int j = 0; j < ((ab & 1) ? 0 : TB); ++j) {
         const int has_flip = csw[j].has_flip, has_pair = csw[j].has_pair;
         if (!(has_flip | has_pair)) continue;
         const int bj = (tid >> j) & 1;
@@ -345,7 +357,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 
       // ---- phase 3: pairs between two thread bits ----
 #pragma unroll 1
-      for (int p = 0; p < n_tt; ++p) {
+      for (int p = 0; p < ((ab & 2) ? 0 : n_tt); ++p) {
         const uint32_t m = ctt[p].mask_lo;
         if (par32((uint32_t)tid & m)) continue;  // rows with x_i == x_j
         const double g = ctt[p].g;
@@ -363,7 +375,9 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 
     // ---- phase 4: the partner tile's contribution ----
     if (pair && !(ab & 128)) {
-      __amdgpu_buffer_rsrc_t src = slot_pa[(k - 1) & 1];
+      // operand of term k: slot k of the partner, or (raw exchange, k = 1) its psi tile
+      const __amdgpu_buffer_rsrc_t src =
+          (xraw && k == 1) ? psi_pa : tile_rsrc(xs_pa + ((size_t)((k - 1) % kXSlots) << L), TBYTES);
       const bool need_flag = xgen || k > 1;  // w_0 of the partner is its psi tile, already visible
       if (need_flag) {
         if (tid == 0 && !(ab & 64)) {
@@ -437,7 +451,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
     for (int r = 0; r < R; ++r) S.w[r * NT + tid] = out[r];
     if (xraw && k < K && !(ab & 64)) {  // w_k for the partner's term k + 1
-      const __amdgpu_buffer_rsrc_t dst = slot_me[k & 1];
+      const __amdgpu_buffer_rsrc_t dst = tile_rsrc(xs_me + ((size_t)(k % kXSlots) << L), TBYTES);
 #pragma unroll
       for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), out[r]);
     }

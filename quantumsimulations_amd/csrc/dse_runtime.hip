@@ -18,6 +18,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -101,9 +102,12 @@ struct dse_ctx {
   int tile_bits = 13;
   int n_streams = 4;
   int persistent = 1;               // use k_interval when every problem fits <= 2 tiles
+  int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
   int n_cu = 256;                   // resident workgroups per launch of the 2-tile kernel
   int* d_flags = nullptr;           // hand-off flags (2 per problem) + error word
   size_t flags_cap = 0;
+  double2* d_xslots = nullptr;      // hand-off slots of the interval kernel
+  size_t xslot_cap = 0;             // in amplitudes
   int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
   double max_degree = 2e6;
@@ -148,6 +152,8 @@ void free_device(dse_ctx* ctx) {
   for (auto& kv : ctx->zzlo_tables) (void)hipFree(kv.second);
   if (ctx->d_flags) (void)hipFree(ctx->d_flags), ctx->d_flags = nullptr;
   ctx->flags_cap = 0;
+  if (ctx->d_xslots) (void)hipFree(ctx->d_xslots), ctx->d_xslots = nullptr;
+  ctx->xslot_cap = 0;
   ctx->zzlo_tables.clear();
   ctx->partial_slots = 0;
   ctx->total_items = 0;
@@ -567,6 +573,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     return ensure_lanes(ctx);
   } else if (k == "persistent") {
     ctx->persistent = value != 0.0;
+  } else if (k == "xcd_pairs") {
+    ctx->xcd_pairs = value != 0.0;
   } else if (k == "time_kernels") {
     if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
     ctx->time_every = (int)value;
@@ -935,7 +943,6 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     d.beta = beta;
     d.s1 = 1.0 / alpha;
   }
-  HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
 
   // ---- execution mode and lanes ----
   // persistent: every problem fits one or two register-block tiles -> one k_interval launch per
@@ -947,6 +954,28 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
     any_dist = any_dist || P.dist;
   }
+  if (persistent) {
+    // hand-off slots of the 2-tile problems: [2 tiles][kXSlots][2^L] amplitudes each
+    // (dse_interval.hip)
+    size_t need = 0;
+    for (auto& P : ctx->probs)
+      if (P.n_tiles == 2) need += (size_t)2 * kXSlots << P.L;
+    if (need > ctx->xslot_cap) {
+      if (ctx->d_xslots) (void)hipFree(ctx->d_xslots), ctx->d_xslots = nullptr;
+      ctx->xslot_cap = 0;
+      if (hipMalloc(&ctx->d_xslots, need * sizeof(double2)) != hipSuccess)
+        return fail(ctx, DSE_ERR_OOM, "hand-off slot allocation failed (" +
+                                          std::to_string(need * sizeof(double2)) + " bytes)");
+      ctx->xslot_cap = need;
+    }
+    size_t off = 0;
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+      const HostProblem& P = ctx->probs[pi];
+      ctx->h_desc[pi].xslots = P.n_tiles == 2 ? ctx->d_xslots + off : nullptr;
+      if (P.n_tiles == 2) off += (size_t)2 * kXSlots << P.L;
+    }
+  }
+  HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
   // dist shards: one lane, so the RCCL exchanges are stream-ordered with every launch
   const int n_lanes = any_dist ? 1 : std::min<int>(ctx->n_streams, (int)ctx->probs.size());
   std::vector<int> order(ctx->probs.size());
@@ -1022,7 +1051,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     const int64_t cap = std::max<int64_t>(2, (ctx->n_cu / 2) * 2);
     for (auto& ln : ctx->lanes)
       for (auto& g : ln.groups) {
-        if (g.tiles != 2) continue;
+        if (g.tiles != 2 || !ctx->xcd_pairs) continue;
         for (int64_t off = 0; off < g.count; off += cap) {
           const int64_t cnt = std::min<int64_t>(cap, g.count - off);
           for (int64_t b0 = 0; b0 < cnt; b0 += 16) {
@@ -1037,7 +1066,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     HIPC(hipMemcpy(ctx->d_items_iv, iv.data(), iv.size() * sizeof(int2), hipMemcpyHostToDevice));
   }
   if (persistent) {
-    const size_t need = 2 * ctx->probs.size() + 1;
+    const size_t need = 2 * ctx->probs.size() + 1;  // flags, error word
     if (ctx->flags_cap < need) {
       if (ctx->d_flags) (void)hipFree(ctx->d_flags), ctx->d_flags = nullptr;
       if (hipMalloc(&ctx->d_flags, need * sizeof(int)) != hipSuccess)

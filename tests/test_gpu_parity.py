@@ -262,3 +262,30 @@ def test_persistent_matches_streaming_and_expm(engine, n, tile_bits):
     psi0[probs[1].psi0_index] = 1.0
     ref = expm_multiply(-1j * t[-1] * sp.csr_matrix(problem_to_csr(probs[1])), psi0)
     assert np.max(np.abs(states[1][1] - ref)) < 1e-10
+
+
+def test_persistent_path_is_bitwise_deterministic(engine):
+    """Repeated evolves of 2-tile problems (cross-workgroup hand-off every term) give identical
+    bits, and agree with the per-term streaming kernels to rounding.  Guards the interval
+    kernel's hand-off protocol and its register budget (a spilling build drifted by ~1e-9)."""
+    t = np.linspace(0.0, 2e-5, 5)
+    params = [sweep_point_params(13, d, v, 2e-5, 5)
+              for d in (0.0, 50e3, 100e3, 150e3) for v in ("center_on", "shell_off")]
+    engine.clear()
+    engine.set_option("tile_bits", 13)
+    for p in params:
+        engine.add(pb.build_problem(p))
+    runs = []
+    for _ in range(3):
+        obs, st = engine.evolve(t)
+        assert st["mode"] == 1
+        runs.append(obs)
+    for o in runs[1:]:
+        assert np.array_equal(o, runs[0])
+    engine.set_option("persistent", 0)
+    try:
+        ref, st = engine.evolve(t)
+        assert st["mode"] == 0
+    finally:
+        engine.set_option("persistent", 1)
+    np.testing.assert_allclose(runs[0], ref, rtol=0, atol=1e-13)
