@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streaming", action="store_true", help="per-term streaming kernels instead of "
                     "the persistent interval kernel")
+    ap.add_argument("--outputs-per-launch", type=int, default=int(os.environ.get("DSE_OUTPUTS_PER_LAUNCH", "2")),
+                    help="persistent mode: output times propagated per launch from one Chebyshev series")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
     ap.add_argument("--n-det", type=int, default=N_DET)
     return ap.parse_args()
@@ -149,6 +151,7 @@ def main():
     eng = Engine(local, tile_bits=args.tile_bits)
     eng.set_option("streams", args.streams)
     eng.set_option("persistent", 0 if args.streaming else 1)
+    eng.set_option("outputs_per_launch", args.outputs_per_launch)
     for p in probs:
         eng.add(p)
 
@@ -227,6 +230,7 @@ def main():
             "engine_mode": "persistent" if mode == 1 else "streaming",
             "tile_bits": args.tile_bits,
             "streams": args.streams,
+            "outputs_per_launch": stats[-1].get("outputs_per_launch"),
             "ms_per_ode_step": (dt / args.steps) / (h_apps / args.steps / len(probs)) * 1e3,
             "h_applications_per_step": h_apps / args.steps,
             "parallelism": f"evolution-sharded x{world} (no collectives)",

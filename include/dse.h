@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 3
+#define DSE_ABI_VERSION 4
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -83,7 +83,7 @@ typedef struct dse_stats {
   int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
   int32_t streams;            /* HIP streams ("lanes") the problems were spread over            */
   int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel   */
-  int32_t reserved;
+  int32_t outputs_per_launch; /* persistent mode: output times per launch (shared series)   */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -107,9 +107,12 @@ void dse_destroy(dse_ctx* ctx);
 const char* dse_last_error(const dse_ctx* ctx);
 /* Options: "tile_bits"    LDS tile, log2 amplitudes per workgroup, 1..13 (default 13)
  *          "streams"      HIP streams the problems are spread over, 1..16 (default 4)
- *          "persistent"   1 (default): one persistent launch per output interval when every
- *                         problem fits one or two LDS tiles (n <= tile_bits + 1); 0: per-term
- *                         streaming launches
+ *          "persistent"   1 (default): one persistent launch per group of output intervals
+ *                         when every problem fits one or two LDS tiles (n <= tile_bits + 1);
+ *                         0: per-term streaming launches
+ *          "outputs_per_launch"  persistent mode: up to this many (1..2) consecutive output
+ *                         times from one Chebyshev series (default 2; 1 on coarse grids,
+ *                         alpha dt >= 400)
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
  *          "max_degree"   Chebyshev degree cap per interval (default 2e6) */

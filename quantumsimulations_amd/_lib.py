@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 3
+DSE_ABI_VERSION = 4
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -49,7 +49,7 @@ class DseStats(C.Structure):
         ("tile_bits", C.c_int32),
         ("streams", C.c_int32),
         ("mode", C.c_int32),
-        ("reserved", C.c_int32),
+        ("outputs_per_launch", C.c_int32),
     ]
 
     def as_dict(self):

@@ -20,6 +20,7 @@ __host__ __device__ constexpr int rr_index(int a, int b) {
   return a * (2 * kRegBits - a - 1) / 2 + (b - a - 1);
 }
 constexpr int kXSlots = 4;                        // hand-off ring of the interval kernel
+constexpr int kMaxOut = 2;                        // output times per interval-kernel launch
 constexpr int kMaxShardBits = 3;                  // partitioned registers: up to 8 shards
 constexpr int kMaxShards = 1 << kMaxShardBits;
 // bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index
@@ -94,6 +95,12 @@ struct DevProb {
   int tbl;                // local tile-index bits: log2(tiles of this shard)
   double2* rbuf[kMaxShards][3];
   double2* xslots;        // interval kernel, 2-tile problems: [2][kXSlots][2^L] hand-off slots
+  // Multi-output launches: one interval-kernel launch propagates n_out <= n_acc consecutive output
+  // times from a shared Chebyshev series.  Output j < n_out - 1 is accumulated in
+  // xacc[j << n_local], the last in the next psi buffer.  Coefficient rows: coef[(set * n_acc + j)
+  // * kcap1 + k].
+  double2* xacc;
+  int n_acc;
 };
 
 // Global tile hp of the role-`role` vector: local buffer or a partner shard's.
@@ -110,7 +117,7 @@ hipError_t set_ablate_interval(int mask);
 bool interval_supported(int L);
 // imag: every drive coefficient of the launched problems is purely imaginary (HostProblem::imag)
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items, int q,
-                           int set, int* flags, int* err, hipStream_t st);
+                           int set, int n_out, int* flags, int* err, hipStream_t st);
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
                       double* partial, hipStream_t st);
 

@@ -102,7 +102,7 @@ __device__ __forceinline__ void sweep_pairs_uniform(const double* g, const doubl
 template <int L, bool IMAG>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
-           int* __restrict__ flags, int* __restrict__ err) {
+           int n_out, int* __restrict__ flags, int* __restrict__ err) {
   constexpr int NT = RB<L>::NT, R = kRegAmps, TB = RB<L>::TB, NH = R / 2;
   constexpr int LANE_BITS = TB < 6 ? TB : 6;
   constexpr uint32_t T = 1u << L;
@@ -138,7 +138,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const cptr<DPair> ctt = cst(P.pairs_tt);
   const cptr<DPair> cph = cst(P.pairs_hi);
   const cptr<DFlip> cfh = cst(P.flips_hi);
-  const cptr<CoefK> ccoef = cst(P.coef + set * P.kcap1);
+  const cptr<CoefK> ccoef = cst(P.coef + (size_t)set * P.n_acc * P.kcap1);  // [j][k] rows
   const int n_tt = P.n_pairs_tt;
   // the top-bit drive (cross flip) for this tile's output bit value (raw exchange)
   double xr = 0.0, xi = 0.0;
@@ -411,41 +411,58 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       }
     }
 
-    // ---- phase 5: recurrence + accumulation (acc operands four registers at a time) ----
-    const cptr<double> cc = (cptr<double>)(ccoef + k);  // c[0..2] as (re, im) pairs
-    const double2 c0 = make_double2(cc[0], cc[1]), c1 = make_double2(cc[2], cc[3]),
-                  c2 = make_double2(cc[4], cc[5]);
-    const bool upd = ccoef[k].upd && !(ab & 256);
+    // ---- phase 5: recurrence, then the propagator sums of the n_out outputs (each updated every
+    // third term from w_{k-2}, w_{k-1}, w_k, and at its own last term) in blocks of AB registers,
+    // every output's accumulator loads of a block in flight together ----
 #pragma unroll
-    for (int r0 = 0; r0 < R; r0 += 4) {
-      double2 accv[4];
-      if (k > 1 && upd) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) accv[r] = bld(acc_t, voff, (uint32_t)((r0 + r) * NT * 16));
+    for (int r = 0; r < R; ++r) {
+      if (k == 1) {
+        out[r].x *= s1;
+        out[r].y *= s1;
+      } else {
+        out[r].x = fma(2.0 * s1, out[r].x, -prev[r].x);
+        out[r].y = fma(2.0 * s1, out[r].y, -prev[r].y);
       }
+    }
+    constexpr int AB = 4;
+    const int nj = (ab & 256) ? 0 : n_out;
+    bool upd[kMaxOut];
+    __amdgpu_buffer_rsrc_t acc_j[kMaxOut];
 #pragma unroll
-      for (int r = r0; r < r0 + 4; ++r) {
-        const double2 own = S.w[r * NT + tid];
-        if (k == 1) {
-          out[r].x *= s1;
-          out[r].y *= s1;
-          double2 a = make_double2(0.0, 0.0);
-          a = cmad(a, c1.x, c1.y, own);
-          a = cmad(a, c2.x, c2.y, out[r]);
-          bst(acc_t, voff, (uint32_t)(r * NT * 16), a);
-        } else {
-          out[r].x = fma(2.0 * s1, out[r].x, -prev[r].x);
-          out[r].y = fma(2.0 * s1, out[r].y, -prev[r].y);
-          if (upd) {
-            double2 a = accv[r - r0];
-            a = cmad(a, c0.x, c0.y, prev[r]);
-            a = cmad(a, c1.x, c1.y, own);
-            a = cmad(a, c2.x, c2.y, out[r]);
-            bst(acc_t, voff, (uint32_t)(r * NT * 16), a);
-          }
+    for (int j = 0; j < kMaxOut; ++j) {
+      upd[j] = j < nj && ccoef[(size_t)j * P.kcap1 + k].upd;
+      acc_j[j] = (j == n_out - 1) ? acc_t
+                                  : tile_rsrc(P.xacc + ((size_t)j << (L + P.tbl)) + (h << L), TBYTES);
+    }
+#pragma unroll
+    for (int r0 = 0; r0 < R; r0 += AB) {
+      double2 ownb[AB];
+#pragma unroll
+      for (int r = 0; r < AB; ++r) ownb[r] = S.w[(r0 + r) * NT + tid];
+      double2 accv[kMaxOut][AB];
+#pragma unroll
+      for (int j = 0; j < kMaxOut; ++j)
+        if (upd[j] && k > 1) {
+#pragma unroll
+          for (int r = 0; r < AB; ++r) accv[j][r] = bld(acc_j[j], voff, (uint32_t)((r0 + r) * NT * 16));
         }
-        prev[r] = own;
+#pragma unroll
+      for (int j = 0; j < kMaxOut; ++j) {
+        if (!upd[j]) continue;
+        const cptr<double> cc = (cptr<double>)(ccoef + (size_t)j * P.kcap1 + k);  // c[0..2] (re, im)
+        const double2 c0 = make_double2(cc[0], cc[1]), c1 = make_double2(cc[2], cc[3]),
+                      c2 = make_double2(cc[4], cc[5]);
+#pragma unroll
+        for (int r = 0; r < AB; ++r) {
+          double2 a = make_double2(0.0, 0.0);
+          if (k > 1) a = cmad(accv[j][r], c0.x, c0.y, prev[r0 + r]);
+          a = cmad(a, c1.x, c1.y, ownb[r]);
+          a = cmad(a, c2.x, c2.y, out[r0 + r]);
+          bst(acc_j[j], voff, (uint32_t)((r0 + r) * NT * 16), a);
+        }
       }
+#pragma unroll
+      for (int r = 0; r < AB; ++r) prev[r0 + r] = ownb[r];
     }
     __syncthreads();  // every read of w_{k-1} in LDS is done
 #pragma unroll
@@ -465,17 +482,17 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 bool interval_supported(int L) { return L >= kRegBlockMinTile && L <= kMaxTile; }
 
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items,
-                           int q, int set, int* flags, int* err, hipStream_t st) {
+                           int q, int set, int n_out, int* flags, int* err, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   switch (L) {
 #define X(l)                                                                                     \
   case l:                                                                                        \
     if (imag)                                                                                    \
       hipLaunchKernelGGL((k_interval<l, true>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs,  \
-                         items, q, set, flags, err);                                             \
+                         items, q, set, n_out, flags, err);                                             \
     else                                                                                         \
       hipLaunchKernelGGL((k_interval<l, false>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs, \
-                         items, q, set, flags, err);                                             \
+                         items, q, set, n_out, flags, err);                                             \
     return hipGetLastError();
     X(10) X(11) X(12) X(13)
 #undef X

@@ -176,7 +176,8 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
   const uint32_t hg = P.h_base | h;
   const int tid = threadIdx.x;
   const bool live = (T >= NT) || (tid < T);
-  const double2* psi = P.buf[bsel];
+  // bsel < 3: a state buffer role; bsel = 3 + j: intermediate output j of a multi-output launch
+  const double2* psi = bsel < 3 ? P.buf[bsel] : P.xacc + ((size_t)(bsel - 3) << (L + P.tbl));
   const size_t base = (size_t)h << L;
 
   double2 own[R];
@@ -219,7 +220,10 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
         }
       } else {
         if ((hg >> (b - L)) & 1u) continue;
-        const double2* src = tile_ptr(P, bsel, hg ^ (1u << (b - L)));
+        const uint32_t hp = hg ^ (1u << (b - L));
+        // intermediate outputs (bsel >= 3) live only in this context, unsharded
+        const double2* src = bsel < 3 ? tile_ptr(P, bsel, hp)
+                                      : psi + ((size_t)(hp & ((1u << P.tbl) - 1u)) << L);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const double2 s = src[r * NT + tid];

@@ -108,6 +108,9 @@ struct dse_ctx {
   size_t flags_cap = 0;
   double2* d_xslots = nullptr;      // hand-off slots of the interval kernel
   size_t xslot_cap = 0;             // in amplitudes
+  double2* d_xacc = nullptr;        // intermediate outputs of multi-output launches
+  size_t xacc_cap = 0;              // in amplitudes
+  int outputs_per_launch = 2;       // M of the interval kernel (dse_evolve picks 1 on coarse grids)
   int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
   double max_degree = 2e6;
@@ -154,6 +157,8 @@ void free_device(dse_ctx* ctx) {
   ctx->flags_cap = 0;
   if (ctx->d_xslots) (void)hipFree(ctx->d_xslots), ctx->d_xslots = nullptr;
   ctx->xslot_cap = 0;
+  if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
+  ctx->xacc_cap = 0;
   ctx->zzlo_tables.clear();
   ctx->partial_slots = 0;
   ctx->total_items = 0;
@@ -573,6 +578,10 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     return ensure_lanes(ctx);
   } else if (k == "persistent") {
     ctx->persistent = value != 0.0;
+  } else if (k == "outputs_per_launch") {
+    if (!(value >= 1 && value <= kMaxOut))
+      return fail(ctx, DSE_ERR_ARG, "outputs_per_launch must be in 1.." + std::to_string(kMaxOut));
+    ctx->outputs_per_launch = (int)value;
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
   } else if (k == "time_kernels") {
@@ -862,73 +871,108 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   int rc = prepare(ctx);
   if (rc) return rc;
 
-  // ---- distinct interval lengths -> coefficient sets ----
-  std::vector<double> set_dt;
-  std::vector<int> set_of(std::max(0, n_t - 1));
-  for (int m = 0; m + 1 < n_t; ++m) {
-    const double dt = t[m + 1] - t[m];
-    int s = -1;
-    for (size_t q = 0; q < set_dt.size(); ++q)
-      if (set_dt[q] == dt) {
-        s = (int)q;
+  // ---- execution mode ----
+  // persistent: every problem fits one or two register-block tiles -> one k_interval launch per
+  // group of output intervals and lane.  streaming: per-term kernels, one output per group.
+  bool persistent = ctx->persistent != 0;
+  bool any_dist = false;
+  for (auto& P : ctx->probs) {
+    if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
+    any_dist = any_dist || P.dist;
+  }
+  // Outputs per launch M: the Chebyshev series of e^{-iH tau} converges after ~ alpha tau +
+  // O((alpha tau)^{1/3}) terms, so M outputs from one series (one propagator sum per output, same
+  // vectors T_k(H~) psi) need fewer H applications than M series of one interval each when alpha
+  // dt is small (the N = 14 sweep on its 1 ms grid: -23% for the stiffest problem at M = 4).  On
+  // coarse grids (alpha dt >= 400) the saving is nil and the coefficient tables grow, so M = 1.
+  double max_z = 0.0;
+  for (int m = 0; m + 1 < n_t; ++m)
+    for (auto& P : ctx->probs) max_z = std::max(max_z, 0.5 * (P.e_max - P.e_min) * (t[m + 1] - t[m]));
+  int M = 1;
+  if (persistent && max_z < 400.0) M = std::max(1, std::min(ctx->outputs_per_launch, n_t - 1));
+
+  // ---- groups of M consecutive output intervals -> coefficient sets (distinct offset lists) ----
+  struct Group {
+    int m0, n_out, set;
+  };
+  std::vector<Group> groups;
+  std::vector<std::vector<double>> set_tau;  // offsets t[m0 + j + 1] - t[m0], j < n_out
+  for (int m0 = 0; m0 + 1 < n_t; m0 += M) {
+    Group g;
+    g.m0 = m0;
+    g.n_out = std::min(M, n_t - 1 - m0);
+    std::vector<double> tau(g.n_out);
+    for (int j = 0; j < g.n_out; ++j) tau[j] = t[m0 + j + 1] - t[m0];
+    g.set = -1;
+    for (size_t q = 0; q < set_tau.size(); ++q)
+      if (set_tau[q] == tau) {
+        g.set = (int)q;
         break;
       }
-    if (s < 0) {
-      if (set_dt.size() >= 4096) return fail(ctx, DSE_ERR_ARG, "more than 4096 distinct output intervals");
-      s = (int)set_dt.size();
-      set_dt.push_back(dt);
+    if (g.set < 0) {
+      if (set_tau.size() >= 4096) return fail(ctx, DSE_ERR_ARG, "more than 4096 distinct output intervals");
+      g.set = (int)set_tau.size();
+      set_tau.push_back(tau);
     }
-    set_of[m] = s;
+    groups.push_back(g);
   }
-  if (set_dt.empty()) set_dt.push_back(0.0);
-  const int n_sets = (int)set_dt.size();
+  if (set_tau.empty()) set_tau.push_back(std::vector<double>(1, 0.0));
+  const int n_sets = (int)set_tau.size();
+  const int n_groups = (int)groups.size();
 
-  // ---- Chebyshev coefficients per problem ----
+  // ---- Chebyshev coefficients per problem: rows [set][output j][term k] ----
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     HostProblem& P = ctx->probs[pi];
     const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
     const double beta = 0.5 * (P.e_max + P.e_min);
     int deg = 1;
-    std::vector<std::vector<double>> J(n_sets);
-    for (int s = 0; s < n_sets; ++s) {
-      const double z = alpha * set_dt[s];
-      const int kmax = (int)std::ceil(z + 12.0 * std::cbrt(z + 1.0) + 60.0);
-      if (kmax > ctx->max_degree)
-        return fail(ctx, DSE_ERR_CONVERGENCE, "Chebyshev degree " + std::to_string(kmax) +
-                                                  " exceeds max_degree; use a finer output grid");
-      J[s].resize(kmax + 1);
-      int d = 1;
-      if (dse_bessel_j(z, kmax, J[s].data(), tol, &d) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
-      deg = std::max(deg, d);
-    }
+    std::vector<std::vector<double>> J((size_t)n_sets * M);
+    std::vector<int> deg_sj((size_t)n_sets * M, 0);
+    for (int s = 0; s < n_sets; ++s)
+      for (size_t j = 0; j < set_tau[s].size(); ++j) {
+        const double z = alpha * set_tau[s][j];
+        const int kmax = (int)std::ceil(z + 12.0 * std::cbrt(z + 1.0) + 60.0);
+        if (kmax > ctx->max_degree)
+          return fail(ctx, DSE_ERR_CONVERGENCE, "Chebyshev degree " + std::to_string(kmax) +
+                                                    " exceeds max_degree; use a finer output grid");
+        std::vector<double>& Jv = J[(size_t)s * M + j];
+        Jv.resize(kmax + 1);
+        int d = 1;
+        if (dse_bessel_j(z, kmax, Jv.data(), tol, &d) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
+        deg_sj[(size_t)s * M + j] = d;
+        deg = std::max(deg, d);
+      }
     P.degree = deg;
     const int kcap1 = deg + 1;
-    std::vector<CoefK> coef((size_t)n_sets * kcap1);
+    std::vector<CoefK> coef((size_t)n_sets * M * kcap1);
     std::memset(coef.data(), 0, coef.size() * sizeof(CoefK));
     std::vector<std::complex<double>> a(deg + 1);
-    for (int s = 0; s < n_sets; ++s) {
-      const double ph = -beta * set_dt[s];
-      const std::complex<double> e(std::cos(ph), std::sin(ph));
-      std::complex<double> mi(1.0, 0.0);  // (-i)^k
-      for (int k = 0; k <= deg; ++k) {
-        const double jk = k < (int)J[s].size() ? J[s][k] : 0.0;
-        a[k] = e * mi * ((k == 0 ? 1.0 : 2.0) * jk);
-        mi *= std::complex<double>(0.0, -1.0);
+    for (int s = 0; s < n_sets; ++s)
+      for (size_t j = 0; j < set_tau[s].size(); ++j) {
+        const std::vector<double>& Jv = J[(size_t)s * M + j];
+        const int dj = deg_sj[(size_t)s * M + j];
+        const double ph = -beta * set_tau[s][j];
+        const std::complex<double> e(std::cos(ph), std::sin(ph));
+        std::complex<double> mi(1.0, 0.0);  // (-i)^k
+        for (int k = 0; k <= deg; ++k) {
+          const double jk = (k <= dj && k < (int)Jv.size()) ? Jv[k] : 0.0;
+          a[k] = e * mi * ((k == 0 ? 1.0 : 2.0) * jk);
+          mi *= std::complex<double>(0.0, -1.0);
+        }
+        auto put = [](double2& d, std::complex<double> v) { d = make_double2(v.real(), v.imag()); };
+        CoefK* row = coef.data() + ((size_t)s * M + j) * kcap1;
+        put(row[1].c[1], a[0]);  // k = 1: acc = a0 w0 + a1 w1
+        put(row[1].c[2], a[1]);
+        row[1].upd = 1;
+        for (int k = 2; k <= dj; ++k) {
+          const int r = (k - 1) % 3;  // regular update every third term covers k-2..k
+          const int nterm = (r == 0) ? 3 : (k == dj ? r : 0);
+          row[k].upd = nterm > 0;
+          if (nterm >= 3) put(row[k].c[0], a[k - 2]);
+          if (nterm >= 2) put(row[k].c[1], a[k - 1]);
+          if (nterm >= 1) put(row[k].c[2], a[k]);
+        }
       }
-      auto put = [](double2& d, std::complex<double> v) { d = make_double2(v.real(), v.imag()); };
-      CoefK* row = coef.data() + (size_t)s * kcap1;
-      put(row[1].c[1], a[0]);  // k = 1: acc = a0 w0 + a1 w1
-      put(row[1].c[2], a[1]);
-      row[1].upd = 1;
-      for (int k = 2; k <= deg; ++k) {
-        const int r = (k - 1) % 3;  // regular update every third term covers k-2..k
-        const int nterm = (r == 0) ? 3 : (k == deg ? r : 0);
-        row[k].upd = nterm > 0;
-        if (nterm >= 3) put(row[k].c[0], a[k - 2]);
-        if (nterm >= 2) put(row[k].c[1], a[k - 1]);
-        if (nterm >= 1) put(row[k].c[2], a[k]);
-      }
-    }
     const size_t cb = coef.size() * sizeof(CoefK);
     if (cb > P.coef_bytes) {
       if (P.coef) (void)hipFree(P.coef), P.coef = nullptr;
@@ -942,18 +986,32 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     d.degree = deg;
     d.beta = beta;
     d.s1 = 1.0 / alpha;
+    d.n_acc = M;
   }
 
-  // ---- execution mode and lanes ----
-  // persistent: every problem fits one or two register-block tiles -> one k_interval launch per
-  // interval and lane; 2-tile problems on lane 0 (their workgroup pairs must be co-resident),
-  // 1-tile problems on lane 1.  streaming: problems by degree dealt round-robin over the lanes.
-  bool persistent = ctx->persistent != 0;
-  bool any_dist = false;
-  for (auto& P : ctx->probs) {
-    if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
-    any_dist = any_dist || P.dist;
+  // intermediate outputs of multi-output launches: (M - 1) state vectors per problem
+  {
+    size_t need = 0;
+    if (M > 1)
+      for (auto& P : ctx->probs) need += (size_t)(M - 1) << P.n_local;
+    if (need > ctx->xacc_cap) {
+      if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
+      ctx->xacc_cap = 0;
+      if (hipMalloc(&ctx->d_xacc, need * sizeof(double2)) != hipSuccess)
+        return fail(ctx, DSE_ERR_OOM, "output accumulator allocation failed (" +
+                                          std::to_string(need * sizeof(double2)) + " bytes)");
+      ctx->xacc_cap = need;
+    }
+    size_t off = 0;
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+      ctx->h_desc[pi].xacc = M > 1 ? ctx->d_xacc + off : nullptr;
+      if (M > 1) off += (size_t)(M - 1) << ctx->probs[pi].n_local;
+    }
   }
+
+  // ---- lanes ----
+  // persistent: 2-tile problems on lane 0 (their workgroup pairs must be co-resident), 1-tile
+  // problems on lane 1.  streaming: problems by degree dealt round-robin over the lanes.
   if (persistent) {
     // hand-off slots of the 2-tile problems: [2 tiles][kXSlots][2^L] amplitudes each
     // (dse_interval.hip)
@@ -1131,11 +1189,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   size_t slot = 0, t_flushed = 0;
   if (any_dist && (rc = dist_exchange(ctx, 0, 0, ctx->lanes[0].stream))) return rc;
   if ((rc = obs_all(0, slot++))) return rc;
-  for (int m = 0; m + 1 < n_t; ++m) {
-    const int q = m & 1;
-    const int set = set_of[m];
-    const bool timed = ctx->time_every > 0 && (m % ctx->time_every) == 0;
-    const int pool = m & 1;
+  for (int gi = 0; gi < n_groups; ++gi) {
+    const Group& G = groups[gi];
+    const int q = gi & 1;
+    const int set = G.set;
+    const bool timed = ctx->time_every > 0 && (gi % ctx->time_every) == 0;
+    const int pool = gi & 1;
     for (size_t li = 0; li < ctx->lanes.size(); ++li) {
       Lane& ln = ctx->lanes[li];
       if (ln.groups.empty()) continue;
@@ -1157,11 +1216,11 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
             if (timed) {
               const size_t i = ln.ev_used[pool]++;
               HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
-              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
+              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out, ctx->d_flags, d_err, ln.stream));
               HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
               pool_bytes[li * 2 + pool].push_back(fl);
             } else {
-              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, ctx->d_flags, d_err, ln.stream));
+              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out, ctx->d_flags, d_err, ln.stream));
             }
             launches += 1.0;
             amp_updates += am;
@@ -1193,13 +1252,16 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         }
       }
     }
-    // new psi of every problem sits in acc(q) = buf[q ? 0 : 2]
+    // new psi of every problem sits in acc(q) = buf[q ? 0 : 2]; outputs j < n_out - 1 of a
+    // multi-output launch in the intermediate accumulators
     if (any_dist && (rc = dist_exchange(ctx, q ? 0 : 2, 0, ctx->lanes[0].stream))) return rc;
-    if ((rc = obs_all(q ? 0 : 2, slot++))) return rc;
-    if (slot == chunk) {
-      if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
-      t_flushed += slot;
-      slot = 0;
+    for (int j = 0; j < G.n_out; ++j) {
+      if ((rc = obs_all(j == G.n_out - 1 ? (q ? 0 : 2) : 3 + j, slot++))) return rc;
+      if (slot == chunk) {
+        if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
+        t_flushed += slot;
+        slot = 0;
+      }
     }
   }
   if (slot > 0) {
@@ -1234,12 +1296,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
                    obs_out + pi * DSE_N_OBS * (size_t)n_t + ti, (size_t)n_t);
     }
   }
-  ctx->last_q = (n_t - 1) & 1;
+  ctx->last_q = n_groups & 1;
   ctx->evolved = true;
 
   if (stats) {
     double happl = 0.0;
-    for (auto& P : ctx->probs) happl += (double)P.degree * (n_t - 1);
+    for (auto& P : ctx->probs) happl += (double)P.degree * n_groups;
     std::memset(stats, 0, sizeof(*stats));
     stats->h_applications = happl;
     stats->amplitude_updates = amp_updates;
@@ -1256,6 +1318,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->n_intervals = n_t - 1;
     stats->tile_bits = ctx->probs.empty() ? 0 : ctx->probs.front().L;
     stats->streams = n_lanes;
+    stats->outputs_per_launch = M;
   }
   return DSE_OK;
 }
