@@ -101,11 +101,13 @@ def lib():
     global _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
+            # DSE_LIB: an alternative build of the same ABI (A/B measurements of kernel variants)
+            path = os.environ.get("DSE_LIB", LIB_PATH)
+            if not os.path.exists(path):
                 raise ImportError(
-                    f"{LIB_PATH} is missing: build it with `python -m quantumsimulations_amd.build` "
+                    f"{path} is missing: build it with `python -m quantumsimulations_amd.build` "
                     "(the HIP engine has no CPU fallback)")
-            handle = C.CDLL(LIB_PATH)
+            handle = C.CDLL(path)
             _declare(handle)
             if handle.dse_abi_version() != DSE_ABI_VERSION:
                 raise ImportError("libdse.so ABI version mismatch; rebuild it")

@@ -36,11 +36,13 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str | None = None) -> str:
+    """Compiles libdse.so (or, with ``out``, a variant library of the same ABI at that path)."""
+    target = out or LIB
+    if not force and out is None and not needs_build():
         return LIB
     hipcc = _hipcc()
-    tmp = LIB + ".tmp"
+    tmp = target + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-Wno-unused-result",
            "-I", os.path.join(ROOT, "include"),
@@ -53,9 +55,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
     if verbose and (res.stdout or res.stderr):
         print(res.stdout + res.stderr)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    out = None
+    if "--out" in sys.argv:
+        out = os.path.abspath(sys.argv[sys.argv.index("--out") + 1])
+    print(build(force="--force" in sys.argv or out is not None, verbose=True, out=out))
