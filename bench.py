@@ -58,6 +58,20 @@ def parse():
     return ap.parse_args()
 
 
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "v6_m2_pmc_traffic.json")
+
+
+def pmc_traffic(kernel: str):
+    """HBM-side bytes per launch of ``kernel`` from the committed rocprofv3 counter passes of this
+    bench command (FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE), or None."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            rec = json.load(f)["kernels"][kernel]
+        return rec["traffic_bytes_per_launch"], os.path.relpath(PMC_TRAFFIC, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def flops_per_amp(prob) -> float:
     """Algorithmic flops per amplitude of one H application:
     diagonal 4, each drive flip 8, each pair 4 on half the rows (= 2 per amp)."""
@@ -181,16 +195,22 @@ def main():
         # persistent interval kernel: the state stays in LDS/registers for all terms of an output
         # interval; HBM moves only psi (once per interval) -> bounded by FP64 VALU throughput
         achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
+        traffic, traffic_src = pmc_traffic("k_interval<13, true>") if args.tile_bits == 13 else (None, None)
         roof = {
             "kernel": "k_interval<13> (persistent Chebyshev interval: all K terms on chip)",
             "bound": "fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": None,
+            "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_rate_gbs": (traffic / (k_ms / k_launches * 1e-3) / 1e9) if (traffic and k_launches) else None,
             "algorithmic_flops_per_amp": fpa,
             "avg_launch_us": k_ms / k_launches * 1e3 if k_launches else None,
             "flops_per_launch": k_flops / k_launches if k_launches else None,
             "aggregate_fp64_tflops": all_flops / dt / 1e12,
-            "note": ("no per-term HBM traffic in this mode; the streaming formulation would move 58.7 B "
-                     "per amplitude per term, i.e. an HBM-equivalent rate of "
+            "note": ("the H terms stay on chip (LDS + registers) for a whole launch, so the bound is FP64 "
+                     "issue (with LDS bandwidth close behind), not HBM; traffic = L2<->fabric bytes per "
+                     "launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes, dominated by the 2-tile "
+                     "problems' per-term hand-off; the streaming formulation would move 58.7 B per "
+                     "amplitude per term, i.e. an HBM-equivalent rate of "
                      f"{all_flops / fpa * 58.7 / dt / 1e9:.0f} GB/s"),
         }
     else:
