@@ -82,7 +82,8 @@ typedef struct dse_stats {
   int32_t n_intervals;        /* output intervals propagated                                    */
   int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
   int32_t streams;            /* HIP streams ("lanes") the problems were spread over            */
-  int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel   */
+  int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel, 
+                                 2: streaming with the Walsh-Hadamard engine                     */
   int32_t outputs_per_launch; /* persistent mode: output times per launch (shared series)   */
 } dse_stats;
 
@@ -113,6 +114,10 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "outputs_per_launch"  persistent mode: up to this many (1..2) consecutive output
  *                         times from one Chebyshev series (default 2; 1 on coarse grids,
  *                         alpha dt >= 400)
+ *          "wht"          1 (default): streaming registers of more than one tile (n >= 14,
+ *                         not sharded) apply H as D_Z + W D_X W + V D_Y V^+ (Walsh-Hadamard
+ *                         passes, two extra state-sized vectors per problem); 0: step kernels
+ *          "wht_group_bits"  high qubits transformed per pass of that engine, 2..11 (default 11)
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
  *          "max_degree"   Chebyshev degree cap per interval (default 2e6) */

@@ -29,6 +29,7 @@
 
 #include "../../include/dse.h"
 #include "dse_internal.h"
+#include "dse_wht.h"
 
 using namespace dse;
 
@@ -60,12 +61,17 @@ struct HostProblem {
   uint32_t xmasks = 0;       // bit m set: terms or observables read shard rank ^ m
   double2* rbuf_own[kMaxShards] = {};  // dist: receive buffers of the exchange, per mask
   bool imag = false;         // every drive coefficient purely imaginary (drive phase pi/2)
+  // Walsh-Hadamard engine (dse_wht.hip): X- and Y-branch vectors and the pair matrix
+  double2* wvec[2] = {nullptr, nullptr};
+  double* d_cquad = nullptr;
+  int wht_groups = 0;        // passes' tile-bit groups; 0: this problem uses the step kernels
 };
 
 // One stream's share of the problems, grouped by tile size.
 struct LaneGroup {
   int L = 0;
   int tiles = 1;            // tiles per problem (persistent mode: 1 or 2)
+  int wht_groups = 0;       // > 0: every problem of the group runs on the Walsh-Hadamard engine
   int64_t off = 0;          // first position in the global item array
   int64_t count = 0;        // items of this group
   std::vector<int> active;     // active[k] = items with degree >= k (prefix of the group)
@@ -102,6 +108,10 @@ struct dse_ctx {
   int tile_bits = 13;
   int n_streams = 4;
   int persistent = 1;               // use k_interval when every problem fits <= 2 tiles
+  int wht = 1;                      // Walsh-Hadamard engine for registers of more tiles
+  int wht_group_bits = 11;          // high bits per pass of that engine (2..11)
+  WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
+  bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
   int n_cu = 256;                   // resident workgroups per launch of the 2-tile kernel
   int* d_flags = nullptr;           // hand-off flags (2 per problem) + error word
@@ -146,8 +156,14 @@ void free_device(dse_ctx* ctx) {
     if (p.d_items) (void)hipFree(p.d_items), p.d_items = nullptr;
     for (auto& b : p.rbuf_own)
       if (b) (void)hipFree(b), b = nullptr;
+    for (auto& b : p.wvec)
+      if (b) (void)hipFree(b), b = nullptr;
+    if (p.d_cquad) (void)hipFree(p.d_cquad), p.d_cquad = nullptr;
+    p.wht_groups = 0;
     p.coef_bytes = 0;
   }
+  if (ctx->d_wht) (void)hipFree(ctx->d_wht), ctx->d_wht = nullptr;
+  ctx->wht_ready = false;
   if (ctx->d_probs) (void)hipFree(ctx->d_probs), ctx->d_probs = nullptr;
   if (ctx->d_items) (void)hipFree(ctx->d_items), ctx->d_items = nullptr;
   if (ctx->d_items_iv) (void)hipFree(ctx->d_items_iv), ctx->d_items_iv = nullptr;
@@ -413,6 +429,81 @@ int prepare(dse_ctx* ctx) {
   return DSE_OK;
 }
 
+// ---- Walsh-Hadamard engine ------------------------------------------------------------------
+// Tile-bit groups of an n-qubit register (WhtGroup): group 0 = bits 0..12; the n - 13 high bits
+// in ceil((n - 13) / max_bits) contiguous, balanced groups, each completed by carried low bits.
+int wht_layout(int n, int max_bits, WhtProb& w) {
+  const int h = n - kWhtTile;
+  if (h < 1 || h > kWhtMaxOuter) return 0;
+  const int ng = (h + max_bits - 1) / max_bits;
+  if (ng + 1 > kWhtMaxGroups) return 0;
+  WhtGroup& g0 = w.grp[0];
+  for (int q = 0; q < kWhtTile; ++q) g0.pos[q] = q;
+  g0.c = 0;
+  g0.n_outer = h;
+  for (int i = 0; i < h; ++i) g0.opos[i] = kWhtTile + i;
+  int first = kWhtTile;
+  for (int gi = 0; gi < ng; ++gi) {
+    const int s = h / ng + (gi < h % ng ? 1 : 0);
+    WhtGroup& g = w.grp[gi + 1];
+    g.c = kWhtTile - s;
+    std::vector<int> in(n, 0);
+    for (int q = 0; q < g.c; ++q) g.pos[q] = q, in[q] = 1;
+    for (int i = 0; i < s; ++i) g.pos[g.c + i] = first + i, in[first + i] = 1;
+    int o = 0;
+    for (int b = 0; b < n; ++b)
+      if (!in[b]) g.opos[o++] = b;
+    g.n_outer = o;
+    first += s;
+  }
+  return ng + 1;
+}
+
+// Builds the engine's tables and vectors for the problems it can take: whole registers (not
+// sharded) of more than one 2^13 tile.  Idempotent until free_device.
+int ensure_wht(dse_ctx* ctx) {
+  if (ctx->wht_ready) return DSE_OK;
+  std::vector<WhtProb> hw(ctx->probs.size());
+  std::memset(hw.data(), 0, hw.size() * sizeof(WhtProb));
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    HostProblem& p = ctx->probs[pi];
+    p.wht_groups = 0;
+    if (!ctx->wht || p.L != kWhtTile || p.n_tiles < 2 || p.shard_bits > 0) continue;
+    const int n = p.n;
+    WhtProb& w = hw[pi];
+    const int G = wht_layout(n, ctx->wht_group_bits, w);
+    if (G < 2) continue;
+    const double sc = std::ldexp(1.0, -n);
+    std::vector<double> cq(size_t(n) * n, 0.0);
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j) cq[size_t(i) * n + j] = cq[size_t(j) * n + i] = 0.5 * p.pair[i * n + j] * sc;
+    for (int b = 0; b < n; ++b) {
+      double re = p.flip[4 * b + 2], im = p.flip[4 * b + 3];
+      if (std::fabs(re) <= 1e-15 * std::hypot(re, im)) re = 0.0;  // as build_tables
+      w.lin_x[b] = re * sc;
+      w.lin_y[b] = im * sc;
+    }
+    const size_t vbytes = (size_t(1) << n) * sizeof(double2);
+    if (hipMalloc(&p.wvec[0], vbytes) != hipSuccess || hipMalloc(&p.wvec[1], vbytes) != hipSuccess ||
+        hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) != hipSuccess)
+      return fail(ctx, DSE_ERR_OOM, "device allocation of the Walsh-Hadamard vectors failed (" +
+                                        std::to_string(2 * vbytes) + " bytes per problem; option wht = 0 "
+                                        "uses the step kernels)");
+    HIPC(hipMemcpy(p.d_cquad, cq.data(), cq.size() * sizeof(double), hipMemcpyHostToDevice));
+    w.vec_a = p.wvec[0];
+    w.vec_b = p.wvec[1];
+    w.cquad = p.d_cquad;
+    w.n = n;
+    w.n_groups = G;
+    p.wht_groups = G;
+  }
+  if (!ctx->d_wht && hipMalloc(&ctx->d_wht, hw.size() * sizeof(WhtProb)) != hipSuccess)
+    return fail(ctx, DSE_ERR_OOM, "device allocation of descriptors failed");
+  HIPC(hipMemcpy(ctx->d_wht, hw.data(), hw.size() * sizeof(WhtProb), hipMemcpyHostToDevice));
+  ctx->wht_ready = true;
+  return DSE_OK;
+}
+
 int ensure_partial(dse_ctx* ctx, size_t slots) {
   if (ctx->partial_slots >= slots) return DSE_OK;
   if (ctx->d_partial) (void)hipFree(ctx->d_partial), ctx->d_partial = nullptr;
@@ -578,6 +669,19 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     return ensure_lanes(ctx);
   } else if (k == "persistent") {
     ctx->persistent = value != 0.0;
+  } else if (k == "wht") {
+    if ((value != 0.0) != (ctx->wht != 0)) {
+      (void)sync_all(ctx);
+      free_device(ctx);
+      ctx->wht = value != 0.0;
+    }
+  } else if (k == "wht_group_bits") {
+    if (!(value >= 2 && value <= 11)) return fail(ctx, DSE_ERR_ARG, "wht_group_bits must be in 2..11");
+    if ((int)value != ctx->wht_group_bits) {
+      (void)sync_all(ctx);
+      free_device(ctx);
+      ctx->wht_group_bits = (int)value;
+    }
   } else if (k == "outputs_per_launch") {
     if (!(value >= 1 && value <= kMaxOut))
       return fail(ctx, DSE_ERR_ARG, "outputs_per_launch must be in 1.." + std::to_string(kMaxOut));
@@ -796,9 +900,13 @@ int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out
     HIPC(hipMemcpyAsync(P.buf[0], in + i * amps, amps * sizeof(double2), hipMemcpyHostToDevice, st));
   }
   if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
+  if ((rc = ensure_wht(ctx))) return rc;
   for (int i = 0; i < count; ++i) {
     HostProblem& P = ctx->probs[first + i];
-    HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+    if (P.wht_groups)
+      HIPC(launch_wht_step(MODE_APPLY, P.wht_groups, ctx->d_wht, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+    else
+      HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
   }
   for (int i = 0; i < count; ++i) {
     HostProblem& P = ctx->probs[first + i];
@@ -879,6 +987,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   for (auto& P : ctx->probs) {
     if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
     any_dist = any_dist || P.dist;
+  }
+  // streaming: registers of more than one 2^13 tile take the Walsh-Hadamard engine (option wht)
+  bool used_wht = false;
+  if (!persistent) {
+    if ((rc = ensure_wht(ctx))) return rc;
+    for (auto& P : ctx->probs) used_wht = used_wht || P.wht_groups > 0;
   }
   // Outputs per launch M: the Chebyshev series of e^{-iH tau} converges after ~ alpha tau +
   // O((alpha tau)^{1/3}) terms, so M outputs from one series (one propagator sum per output, same
@@ -1072,6 +1186,9 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         ln.max_deg = std::max(ln.max_deg, ctx->probs[pi].degree);
       }
       g.count = (int64_t)items.size() - g.off;
+      g.wht_groups = persistent ? 0 : ctx->probs[kv.second.front()].wht_groups;
+      for (int pi : kv.second)
+        if (ctx->probs[pi].wht_groups != g.wht_groups) g.wht_groups = 0;
       const int gdeg = ctx->probs[kv.second.front()].degree;
       g.active.assign(gdeg + 2, 0);
       g.bytes.assign(gdeg + 2, 0.0);
@@ -1229,7 +1346,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
           continue;
         }
         if (any_dist && (rc = dist_exchange(ctx, q ? 2 : 0, 1, ln.stream))) return rc;
-        HIPC(launch_step(g.L, MODE_FIRST, ctx->d_probs, ctx->d_items + g.off, g.active[1], 1, q, set, ln.stream));
+        auto step = [&](int mode, int na, int k) {
+          return g.wht_groups ? launch_wht_step(mode, g.wht_groups, ctx->d_wht, ctx->d_probs, ctx->d_items + g.off,
+                                                na, k, q, set, ln.stream)
+                              : launch_step(g.L, mode, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream);
+        };
+        HIPC(step(MODE_FIRST, g.active[1], 1));
         for (int k = 2; k < (int)g.active.size(); ++k) {
           const int na = g.active[k];
           if (na <= 0) break;
@@ -1238,12 +1360,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
           if (timed) {
             const size_t i = ln.ev_used[pool]++;
             HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
-            HIPC(launch_step(g.L, MODE_GEN, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
+            HIPC(step(MODE_GEN, na, k));
             HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
             pool_bytes[li * 2 + pool].push_back(g.flops[k]);
             pool_bytes2[li * 2 + pool].push_back(g.bytes[k]);
           } else {
-            HIPC(launch_step(g.L, MODE_GEN, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
+            HIPC(step(MODE_GEN, na, k));
           }
           launches += 1.0;
           amp_updates += (double)na * T;
@@ -1308,7 +1430,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->step_bytes = all_bytes;
     stats->h_flops = all_flops;
     stats->timed_flops = flops_timed;
-    stats->mode = persistent ? 1 : 0;
+    stats->mode = persistent ? 1 : (used_wht ? 2 : 0);
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
     stats->step_launches = launches;
     stats->timed_launches = launches_timed;

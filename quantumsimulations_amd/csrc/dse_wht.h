@@ -1,0 +1,43 @@
+// dse_wht.h -- descriptors of the Walsh-Hadamard engine (dse_wht.hip): H|w> for registers of
+// more than two tiles as D_Z + W D_X W + V D_Y V^+ in a few streaming passes over HBM.
+#pragma once
+
+#include "dse_internal.h"
+
+namespace dse {
+
+enum { WHT_FIRST = 0, WHT_FWD = 1, WHT_MID = 2, WHT_INV = 3, WHT_FINAL = 4 };
+
+constexpr int kWhtTile = 13;                          // tile bits of every pass
+constexpr int kWhtMaxGroups = 4;                      // group 0 + up to 3 high groups
+constexpr int kWhtMaxOuter = DSE_MAX_HIGH_BITS(13);   // 21 outer bits at 34 qubits
+constexpr int kWhtMaxQubits = 34;
+
+// Tile bit q of a group-g tile is global bit pos[q]; outer index bit i is global bit opos[i].
+// Group 0: pos = 0..12.  High groups: pos[0..c-1] = 0..c-1 (carried, not transformed in this
+// pass: contiguous 2^c-amplitude runs keep the loads coalesced), pos[c..12] = the group's bits.
+struct WhtGroup {
+  int pos[kWhtTile];
+  int c;
+  int n_outer;
+  int opos[kWhtMaxOuter];
+};
+
+struct WhtProb {
+  double2* vec_a;         // W-basis image of w (X branch)
+  double2* vec_b;         // V-basis image of w (Y branch)
+  const double* cquad;    // [n*n] symmetric: (pair_ij / 2) * 2^-n, zero diagonal
+  double lin_x[kWhtMaxQubits];  // Re c_1 of the drive of bit b, * 2^-n
+  double lin_y[kWhtMaxQubits];  // Im c_1, * 2^-n
+  int n;
+  int n_groups;
+  WhtGroup grp[kWhtMaxGroups];
+};
+
+// One H application (mode MODE_APPLY) or one Chebyshev term (MODE_FIRST / MODE_GEN, buffer
+// roles and coefficient rows as launch_step) over items (problem, tile index): n_groups passes
+// FIRST, FWD x (G - 2), MID, INV x (G - 2), FINAL.  Every item's problem must have P.L == 13.
+hipError_t launch_wht_step(int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
+                           const int2* items, int n_items, int k, int q, int set, hipStream_t st);
+
+}  // namespace dse

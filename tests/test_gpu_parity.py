@@ -252,7 +252,7 @@ def test_persistent_matches_streaming_and_expm(engine, n, tile_bits):
             for p in probs:
                 engine.add(p)
             res[pers], st = engine.evolve(t)
-            assert st["mode"] == pers
+            assert st["mode"] == (1 if pers else (2 if tile_bits == 13 and n > 13 else 0))
             states[pers] = [engine.state(i) for i in range(len(probs))]
     finally:
         engine.set_option("persistent", 1)
@@ -283,9 +283,14 @@ def test_persistent_path_is_bitwise_deterministic(engine):
     for o in runs[1:]:
         assert np.array_equal(o, runs[0])
     engine.set_option("persistent", 0)
+    engine.set_option("wht", 0)
     try:
+        engine.clear()
+        for p in params:
+            engine.add(pb.build_problem(p))
         ref, st = engine.evolve(t)
         assert st["mode"] == 0
     finally:
         engine.set_option("persistent", 1)
+        engine.set_option("wht", 1)
     np.testing.assert_allclose(runs[0], ref, rtol=0, atol=1e-13)

@@ -1,0 +1,104 @@
+"""GPU parity of the Walsh-Hadamard engine (csrc/dse_wht.hip, option "wht").
+
+H|psi> = D_Z psi + W D_X W psi + V D_Y V^+ psi over LDS-tiled passes; the H is the same as the
+step kernels' term tables, so the checks are
+  H|psi>          vs the oracle's bitwise H (rel 1e-13 of max|H psi|), n <= 20, every pass count
+                  G = 2, 3, 4 and carried-bit count of the group layout
+  H|psi>          vs the step kernels (wht = 0) at n = 22, 24 (rel 1e-13): both validated above
+  time traces     vs the step kernels (atol 1e-11) and the final state vs expm_multiply (1e-10)
+"""
+import numpy as np
+import pytest
+
+from oracle import reference_model as rm
+
+from test_gpu_parity import _rand, _random_problem, _tables
+
+pytestmark = pytest.mark.gpu
+
+
+def _apply(engine, prob, v, **opts):
+    engine.clear()
+    for k, val in opts.items():
+        engine.set_option(k, val)
+    try:
+        pid = engine.add(prob)
+        return engine.apply_h(pid, v)
+    finally:
+        engine.set_option("wht", 1)
+        engine.set_option("wht_group_bits", 11)
+
+
+# n, group bits -> high groups of sizes (carried bits c = 13 - size)
+@pytest.mark.parametrize("n,gbits", [(14, 11), (15, 11), (17, 11), (17, 2), (20, 11), (20, 4),
+                                     (20, 3), (19, 9)])
+def test_wht_apply_matches_oracle(engine, n, gbits):
+    prob = _random_problem(n, 700 + n + gbits)
+    v = _rand(n, 7 + n)
+    out = _apply(engine, prob, v, wht=1, wht_group_bits=gbits)
+    ref = rm.bitwise_apply(_tables(prob), v)
+    assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("n", [22, 24])
+def test_wht_apply_matches_step_kernels(engine, n):
+    prob = _random_problem(n, 900 + n)
+    v = _rand(n, 11 + n)
+    a = _apply(engine, prob, v, wht=1)
+    b = _apply(engine, prob, v, wht=0)
+    assert np.max(np.abs(a - b)) <= 1e-13 * np.max(np.abs(b))
+
+
+def test_wht_sweep_problem_imaginary_drive(engine):
+    """A sweep point (drive phase pi/2: purely imaginary flips, rare bit driven) at N = 15."""
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.sweep import sweep_point_params
+    prob = pb.build_problem(sweep_point_params(14, 50e3, "center_on", 1e-5, 3))
+    v = _rand(prob.n_qubits, 3)
+    out = _apply(engine, prob, v, wht=1)
+    ref = rm.bitwise_apply(_tables(prob), v)
+    assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
+
+
+def test_wht_evolve_matches_step_kernels_and_expm(engine):
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import expm_multiply
+    from quantumsimulations_amd.dipolar_ensemble_with_rare import problem_to_csr
+    n = 16
+    probs = [_random_problem(n, 1300 + s, rare_bit=n - 1) for s in range(3)]
+    probs[2].field[:] *= 3.0  # a different spectral width -> a different Chebyshev degree
+    t = np.linspace(0.0, 4e-4, 5)
+    res, states = {}, {}
+    try:
+        for wht in (0, 1):
+            engine.clear()
+            engine.set_option("wht", wht)
+            for p in probs:
+                engine.add(p)
+            res[wht], st = engine.evolve(t)
+            assert st["mode"] == (2 if wht else 0)
+            states[wht] = [engine.state(i) for i in range(len(probs))]
+    finally:
+        engine.set_option("wht", 1)
+    np.testing.assert_allclose(res[1], res[0], rtol=0, atol=1e-11)
+    psi0 = np.zeros(1 << n, dtype=complex)
+    psi0[probs[2].psi0_index] = 1.0
+    ref = expm_multiply(-1j * t[-1] * sp.csr_matrix(problem_to_csr(probs[2])), psi0)
+    assert np.max(np.abs(states[1][2] - ref)) < 1e-10
+
+
+def test_wht_not_used_for_small_tiles_or_persistent(engine):
+    prob = _random_problem(16, 5)
+    t = np.linspace(0.0, 1e-4, 3)
+    engine.clear()
+    engine.set_option("tile_bits", 12)
+    try:
+        engine.add(prob)
+        _, st = engine.evolve(t)
+        assert st["mode"] == 0
+    finally:
+        engine.set_option("tile_bits", 13)
+    engine.clear()
+    engine.add(_random_problem(13, 6))
+    _, st = engine.evolve(t)
+    assert st["mode"] == 1
