@@ -64,6 +64,7 @@ struct HostProblem {
   // Walsh-Hadamard engine (dse_wht.hip): X- and Y-branch vectors and the pair matrix
   double2* wvec[2] = {nullptr, nullptr};
   double* d_cquad = nullptr;
+  double* d_wtab = nullptr;  // ztab | xytab
   int wht_groups = 0;        // passes' tile-bit groups; 0: this problem uses the step kernels
 };
 
@@ -159,6 +160,7 @@ void free_device(dse_ctx* ctx) {
     for (auto& b : p.wvec)
       if (b) (void)hipFree(b), b = nullptr;
     if (p.d_cquad) (void)hipFree(p.d_cquad), p.d_cquad = nullptr;
+    if (p.d_wtab) (void)hipFree(p.d_wtab), p.d_wtab = nullptr;
     p.wht_groups = 0;
     p.coef_bytes = 0;
   }
@@ -485,7 +487,8 @@ int ensure_wht(dse_ctx* ctx) {
     }
     const size_t vbytes = (size_t(1) << n) * sizeof(double2);
     if (hipMalloc(&p.wvec[0], vbytes) != hipSuccess || hipMalloc(&p.wvec[1], vbytes) != hipSuccess ||
-        hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) != hipSuccess)
+        hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) != hipSuccess ||
+        hipMalloc(&p.d_wtab, (size_t)p.n_tiles * 48 * sizeof(double)) != hipSuccess)
       return fail(ctx, DSE_ERR_OOM, "device allocation of the Walsh-Hadamard vectors failed (" +
                                         std::to_string(2 * vbytes) + " bytes per problem; option wht = 0 "
                                         "uses the step kernels)");
@@ -493,6 +496,8 @@ int ensure_wht(dse_ctx* ctx) {
     w.vec_a = p.wvec[0];
     w.vec_b = p.wvec[1];
     w.cquad = p.d_cquad;
+    w.ztab = p.d_wtab;
+    w.xytab = p.d_wtab + (size_t)p.n_tiles * 16;
     w.n = n;
     w.n_groups = G;
     p.wht_groups = G;
@@ -500,6 +505,10 @@ int ensure_wht(dse_ctx* ctx) {
   if (!ctx->d_wht && hipMalloc(&ctx->d_wht, hw.size() * sizeof(WhtProb)) != hipSuccess)
     return fail(ctx, DSE_ERR_OOM, "device allocation of descriptors failed");
   HIPC(hipMemcpy(ctx->d_wht, hw.data(), hw.size() * sizeof(WhtProb), hipMemcpyHostToDevice));
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+    if (ctx->probs[pi].wht_groups)
+      HIPC(launch_wht_tables(ctx->d_wht + pi, ctx->d_probs + pi, ctx->probs[pi].n_tiles, ctx->lanes[0].stream));
+  HIPC(hipStreamSynchronize(ctx->lanes[0].stream));
   ctx->wht_ready = true;
   return DSE_OK;
 }

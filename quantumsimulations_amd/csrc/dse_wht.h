@@ -27,12 +27,18 @@ struct WhtProb {
   double2* vec_a;         // W-basis image of w (X branch)
   double2* vec_b;         // V-basis image of w (Y branch)
   const double* cquad;    // [n*n] symmetric: (pair_ij / 2) * 2^-n, zero diagonal
+  // per-tile coefficient tables (launch_wht_tables), one row per outer index o:
+  double* ztab;           // [tiles][16] group 0: F_i(o) i < 13, C(o) without beta (D_Z, s = 1/2 - bit)
+  double* xytab;          // [tiles][32] MID group: F^X_q(o), C^X(o) at 0..13, F^Y, C^Y at 16..29
   double lin_x[kWhtMaxQubits];  // Re c_1 of the drive of bit b, * 2^-n
   double lin_y[kWhtMaxQubits];  // Im c_1, * 2^-n
   int n;
   int n_groups;
   WhtGroup grp[kWhtMaxGroups];
 };
+
+// Fills ztab / xytab of problem wp (device pointers to one WhtProb / DevProb entry).
+hipError_t launch_wht_tables(const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st);
 
 // One H application (mode MODE_APPLY) or one Chebyshev term (MODE_FIRST / MODE_GEN, buffer
 // roles and coefficient rows as launch_step) over items (problem, tile index): n_groups passes

@@ -161,49 +161,18 @@ __device__ __forceinline__ void tile_full(double2* lds, double2* v, int c, int t
 
 struct WhtShared {
   double2 w[WT + 2 * (WT >> 5)];  // padded slots (slot_base)
-  double fx[WL + 1], fy[WL + 1];  // per-tile linear coefficients of D_X, D_Y (index WL: constant)
+  double fx[WL + 1], fy[WL + 1];  // per-tile linear coefficients of D_X, D_Y (index WL: constant; xytab)
   double cq[WL * WL];             // in-tile couplings c(q, q'), symmetric (D_X sign)
   double zr[WR];                  // register-register part of D_X in the MID layout
-  double cz[WL + 1];              // D_Z of a group-0 tile: F_i(h), C(h) (tile_diag_coeffs)
+  double cz[WL + 1];              // D_Z of a group-0 tile: F_i(h), C(h) - beta (ztab)
 };
 
 __device__ __forceinline__ double zsign(uint64_t v, int b) { return ((v >> b) & 1ull) ? -1.0 : 1.0; }
 
-// Per-tile coefficients of D_X and D_Y: F_q = lin(pos_q) + sum_o c(pos_q, o) z_o, constant
-// C = sum_o lin(o) z_o + sum_{o<o'} c(o, o') z_o z_o' (D_Y: lin_y and -c).  No barrier.
-__device__ void tile_xy_coeffs(const WhtProb& W, const WhtGroup& G, uint64_t o, WhtShared& S, int tid) {
-  const int n = W.n;
+// In-tile couplings c(pos_q, pos_q') of a group (same for all its tiles).  No barrier.
+__device__ __forceinline__ void stage_couplings(const WhtProb& W, const WhtGroup& G, WhtShared& S, int tid) {
   const gdbl* cq = gptr(W.cquad);
-  if (tid < WL) {
-    const int b = G.pos[tid];
-    double fx = W.lin_x[b], fy = W.lin_y[b];
-    for (int i = 0; i < G.n_outer; ++i) {
-      const double c = cq[b * n + G.opos[i]] * zsign(o, i);
-      fx += c;
-      fy -= c;
-    }
-    S.fx[tid] = fx;
-    S.fy[tid] = fy;
-  } else if (tid == WL) {
-    double cx = 0.0, cy = 0.0;
-    for (int i = 0; i < G.n_outer; ++i) {
-      const int bi = G.opos[i];
-      const double zi = zsign(o, i);
-      cx += W.lin_x[bi] * zi;
-      cy += W.lin_y[bi] * zi;
-      for (int j = i + 1; j < G.n_outer; ++j) {
-        const double c = cq[bi * n + G.opos[j]] * (zi * zsign(o, j));
-        cx += c;
-        cy -= c;
-      }
-    }
-    S.fx[WL] = cx;
-    S.fy[WL] = cy;
-  }
-  for (int e = tid; e < WL * WL; e += WNT) {
-    const int a = e / WL, b = e % WL;
-    S.cq[e] = cq[G.pos[a] * n + G.pos[b]];
-  }
+  for (int e = tid; e < WL * WL; e += WNT) S.cq[e] = cq[G.pos[e / WL] * W.n + G.pos[e % WL]];
 }
 
 // zr[r] of layout lay (needs S.cq after a barrier)
@@ -320,7 +289,12 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   if (PASS == WHT_FWD || PASS == WHT_INV || PASS == WHT_MID) {
     const int lm = last_layout(G.c);
     if (PASS == WHT_MID) {
-      tile_xy_coeffs(W, G, o, S, tid);
+      stage_couplings(W, G, S, tid);
+      if (tid < 32) {
+        const double c = gptr((const double*)W.xytab)[o * 32 + tid];
+        if (tid <= WL) S.fx[tid] = c;
+        else if (tid >= 16 && tid <= 16 + WL) S.fy[tid - 16] = c;
+      }
       __syncthreads();
       tile_zr(S, lm, tid);  // read after the first transpose's barriers
     }
@@ -346,7 +320,10 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   // ---- FINAL (group 0 tile = ordinary tile h): out = D_Z w + W0 A + S W0 B, then the recurrence
   if (PASS == WHT_FINAL) {
     const uint32_t h = (uint32_t)o;
-    tile_diag_coeffs<WL>(P, h, MODE == MODE_APPLY ? 0.0 : P.beta, S.cz, tid);
+    if (tid <= WL) {
+      const double c = gptr((const double*)W.ztab)[(uint64_t)h * 16 + tid];
+      S.cz[tid] = (tid == WL && MODE != MODE_APPLY) ? c - P.beta : c;
+    }
     double2 out[WR];
     const gd2* B = gptr((const double2*)W.vec_b);
 #pragma unroll
@@ -390,6 +367,61 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   }
 }
 
+// One thread per tile o: D_Z pieces of group-0 tile o (tile_diag_coeffs without beta) and the
+// D_X / D_Y pieces of MID-group tile o:  F_q = lin(pos_q) + sum_i c(pos_q, opos_i) z_i,
+// C = sum_i lin(opos_i) z_i + sum_{i<j} c(opos_i, opos_j) z_i z_j  (D_Y: lin_y, -c).
+__global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ wp, const DevProb* __restrict__ dp,
+                                                    int64_t tiles) {
+  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= tiles) return;
+  const WhtProb& W = *wp;
+  const DevProb& P = *dp;
+  const int n = W.n;
+  double* zt = W.ztab + o * 16;
+  for (int i = 0; i < WL; ++i) {
+    double f = P.field[i];
+    for (int j = WL; j < n; ++j) f += P.zz[i * n + j] * (0.5 - (double)((o >> (j - WL)) & 1));
+    zt[i] = f;
+  }
+  double c = P.shift;
+  for (int j = WL; j < n; ++j) {
+    const double sj = 0.5 - (double)((o >> (j - WL)) & 1);
+    c += P.field[j] * sj;
+    for (int i = WL; i < j; ++i) c += P.zz[i * n + j] * ((0.5 - (double)((o >> (i - WL)) & 1)) * sj);
+  }
+  zt[WL] = c;
+  zt[WL + 1] = zt[WL + 2] = 0.0;
+  const WhtGroup& G = W.grp[W.n_groups - 1];
+  const double* cq = W.cquad;
+  double* xy = W.xytab + o * 32;
+  for (int q = 0; q < WL; ++q) {
+    const int b = G.pos[q];
+    double fx = W.lin_x[b], fy = W.lin_y[b];
+    for (int i = 0; i < G.n_outer; ++i) {
+      const double v = cq[b * n + G.opos[i]] * zsign(o, i);
+      fx += v;
+      fy -= v;
+    }
+    xy[q] = fx;
+    xy[16 + q] = fy;
+  }
+  double cx = 0.0, cy = 0.0;
+  for (int i = 0; i < G.n_outer; ++i) {
+    const int bi = G.opos[i];
+    const double zi = zsign(o, i);
+    cx += W.lin_x[bi] * zi;
+    cy += W.lin_y[bi] * zi;
+    for (int j = i + 1; j < G.n_outer; ++j) {
+      const double v = cq[bi * n + G.opos[j]] * (zi * zsign(o, j));
+      cx += v;
+      cy -= v;
+    }
+  }
+  xy[WL] = cx;
+  xy[16 + WL] = cy;
+  xy[14] = xy[15] = xy[30] = xy[31] = 0.0;
+}
+
 template <int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
                        int g, int k, int q, int set, hipStream_t st) {
@@ -404,6 +436,11 @@ hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int
 }
 
 }  // namespace
+
+hipError_t launch_wht_tables(const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st) {
+  hipLaunchKernelGGL(k_wht_tables, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, st, wp, dp, tiles);
+  return hipGetLastError();
+}
 
 hipError_t launch_wht_step(int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
                            const int2* items, int n_items, int k, int q, int set, hipStream_t st) {
