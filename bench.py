@@ -166,6 +166,8 @@ def main():
     eng.set_option("streams", args.streams)
     eng.set_option("persistent", 0 if args.streaming else 1)
     eng.set_option("outputs_per_launch", args.outputs_per_launch)
+    if os.environ.get("DSE_CORESIDENT"):  # diagnostics: workgroups per 2-tile interval launch chunk
+        eng.set_option("coresident", float(os.environ["DSE_CORESIDENT"]))
     for p in probs:
         eng.add(p)
 

@@ -695,6 +695,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     if (!(value >= 1 && value <= kMaxOut))
       return fail(ctx, DSE_ERR_ARG, "outputs_per_launch must be in 1.." + std::to_string(kMaxOut));
     ctx->outputs_per_launch = (int)value;
+  } else if (k == "coresident") {  // diagnostics: workgroups per chunk of a 2-tile interval launch
+    if (!(value >= 2 && value <= 4096)) return fail(ctx, DSE_ERR_ARG, "coresident must be in 2..4096");
+    ctx->n_cu = (int)value;
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
   } else if (k == "time_kernels") {

@@ -102,3 +102,14 @@ def test_wht_not_used_for_small_tiles_or_persistent(engine):
     engine.add(_random_problem(13, 6))
     _, st = engine.evolve(t)
     assert st["mode"] == 1
+
+
+def test_wht_evolve_is_bitwise_deterministic(engine):
+    """Repeated evolves on the engine give identical bits (no atomics, fixed reduction order)."""
+    prob = _random_problem(17, 4321, rare_bit=16)
+    t = np.linspace(0.0, 1e-4, 4)
+    engine.clear()
+    engine.add(prob)
+    runs = [engine.evolve(t)[0] for _ in range(2)]
+    assert np.array_equal(runs[0], runs[1])
+    assert np.array_equal(engine.state(0), engine.state(0))
