@@ -110,7 +110,8 @@ struct dse_ctx {
   int n_streams = 4;
   int persistent = 1;               // use k_interval when every problem fits <= 2 tiles
   int wht = 1;                      // Walsh-Hadamard engine for registers of more tiles
-  int wht_group_bits = 11;          // high bits per pass of that engine (2..11)
+  int wht_group_bits = 0;           // high bits per pass of that engine (0: tile bits - 2)
+  int wht_tile_bits = 0;            // its tile: 12, 13, 0 = 13 up to 24 qubits, else 12
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
@@ -211,7 +212,10 @@ int sync_all(dse_ctx* ctx) {
 int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
   const int n = p.n;
   const int nl = p.n_local;   // qubits held in this context (n unless partitioned)
-  const int L = std::max(std::min(nl, ctx->tile_bits), std::max(kMinTile, nl - 32));
+  int L = std::max(std::min(nl, ctx->tile_bits), std::max(kMinTile, nl - 32));
+  // registers for the Walsh-Hadamard engine (whole, more than two 2^13 tiles) take its tile size
+  if (ctx->wht && ctx->tile_bits == kMaxTile && p.shard_bits == 0 && nl > kMaxTile + 1)
+    L = ctx->wht_tile_bits ? ctx->wht_tile_bits : (nl <= 24 ? 13 : 12);
   if (L > kMaxTile) return fail(ctx, DSE_ERR_ARG, "problem too large for the tile range");
   p.L = L;
   p.n_tiles = int64_t(1) << (nl - L);
@@ -434,21 +438,21 @@ int prepare(dse_ctx* ctx) {
 // ---- Walsh-Hadamard engine ------------------------------------------------------------------
 // Tile-bit groups of an n-qubit register (WhtGroup): group 0 = bits 0..12; the n - 13 high bits
 // in ceil((n - 13) / max_bits) contiguous, balanced groups, each completed by carried low bits.
-int wht_layout(int n, int max_bits, WhtProb& w) {
-  const int h = n - kWhtTile;
+int wht_layout(int n, int wl, int max_bits, WhtProb& w) {
+  const int h = n - wl;
   if (h < 1 || h > kWhtMaxOuter) return 0;
   const int ng = (h + max_bits - 1) / max_bits;
   if (ng + 1 > kWhtMaxGroups) return 0;
   WhtGroup& g0 = w.grp[0];
-  for (int q = 0; q < kWhtTile; ++q) g0.pos[q] = q;
+  for (int q = 0; q < wl; ++q) g0.pos[q] = q;
   g0.c = 0;
   g0.n_outer = h;
-  for (int i = 0; i < h; ++i) g0.opos[i] = kWhtTile + i;
-  int first = kWhtTile;
+  for (int i = 0; i < h; ++i) g0.opos[i] = wl + i;
+  int first = wl;
   for (int gi = 0; gi < ng; ++gi) {
     const int s = h / ng + (gi < h % ng ? 1 : 0);
     WhtGroup& g = w.grp[gi + 1];
-    g.c = kWhtTile - s;
+    g.c = wl - s;
     std::vector<int> in(n, 0);
     for (int q = 0; q < g.c; ++q) g.pos[q] = q, in[q] = 1;
     for (int i = 0; i < s; ++i) g.pos[g.c + i] = first + i, in[first + i] = 1;
@@ -470,10 +474,11 @@ int ensure_wht(dse_ctx* ctx) {
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     HostProblem& p = ctx->probs[pi];
     p.wht_groups = 0;
-    if (!ctx->wht || p.L != kWhtTile || p.n_tiles < 2 || p.shard_bits > 0) continue;
+    if (!ctx->wht || p.L < kWhtMinTile || p.L > kWhtMaxTile || p.n_tiles < 2 || p.shard_bits > 0) continue;
     const int n = p.n;
     WhtProb& w = hw[pi];
-    const int G = wht_layout(n, ctx->wht_group_bits, w);
+    const int gb = ctx->wht_group_bits ? std::min(ctx->wht_group_bits, p.L - 2) : p.L - 2;
+    const int G = wht_layout(n, p.L, gb, w);
     if (G < 2) continue;
     const double sc = std::ldexp(1.0, -n);
     std::vector<double> cq(size_t(n) * n, 0.0);
@@ -499,6 +504,7 @@ int ensure_wht(dse_ctx* ctx) {
     w.ztab = p.d_wtab;
     w.xytab = p.d_wtab + (size_t)p.n_tiles * 16;
     w.n = n;
+    w.wl = p.L;
     w.n_groups = G;
     p.wht_groups = G;
   }
@@ -507,7 +513,7 @@ int ensure_wht(dse_ctx* ctx) {
   HIPC(hipMemcpy(ctx->d_wht, hw.data(), hw.size() * sizeof(WhtProb), hipMemcpyHostToDevice));
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
     if (ctx->probs[pi].wht_groups)
-      HIPC(launch_wht_tables(ctx->d_wht + pi, ctx->d_probs + pi, ctx->probs[pi].n_tiles, ctx->lanes[0].stream));
+      HIPC(launch_wht_tables(ctx->probs[pi].L, ctx->d_wht + pi, ctx->d_probs + pi, ctx->probs[pi].n_tiles, ctx->lanes[0].stream));
   HIPC(hipStreamSynchronize(ctx->lanes[0].stream));
   ctx->wht_ready = true;
   return DSE_OK;
@@ -684,8 +690,16 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
       free_device(ctx);
       ctx->wht = value != 0.0;
     }
+  } else if (k == "wht_tile_bits") {
+    if (!(value == 0 || value == 12 || value == 13)) return fail(ctx, DSE_ERR_ARG, "wht_tile_bits must be 0, 12 or 13");
+    if ((int)value != ctx->wht_tile_bits) {
+      (void)sync_all(ctx);
+      free_device(ctx);
+      ctx->wht_tile_bits = (int)value;
+    }
   } else if (k == "wht_group_bits") {
-    if (!(value >= 2 && value <= 11)) return fail(ctx, DSE_ERR_ARG, "wht_group_bits must be in 2..11");
+    if (!(value == 0 || (value >= 2 && value <= 11)))
+      return fail(ctx, DSE_ERR_ARG, "wht_group_bits must be 0 or in 2..11");
     if ((int)value != ctx->wht_group_bits) {
       (void)sync_all(ctx);
       free_device(ctx);
@@ -916,7 +930,7 @@ int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out
   for (int i = 0; i < count; ++i) {
     HostProblem& P = ctx->probs[first + i];
     if (P.wht_groups)
-      HIPC(launch_wht_step(MODE_APPLY, P.wht_groups, ctx->d_wht, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+      HIPC(launch_wht_step(P.L, MODE_APPLY, P.wht_groups, ctx->d_wht, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
     else
       HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
   }
@@ -1359,7 +1373,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         }
         if (any_dist && (rc = dist_exchange(ctx, q ? 2 : 0, 1, ln.stream))) return rc;
         auto step = [&](int mode, int na, int k) {
-          return g.wht_groups ? launch_wht_step(mode, g.wht_groups, ctx->d_wht, ctx->d_probs, ctx->d_items + g.off,
+          return g.wht_groups ? launch_wht_step(g.L, mode, g.wht_groups, ctx->d_wht, ctx->d_probs, ctx->d_items + g.off,
                                                 na, k, q, set, ln.stream)
                               : launch_step(g.L, mode, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream);
         };

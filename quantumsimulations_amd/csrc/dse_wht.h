@@ -8,16 +8,17 @@ namespace dse {
 
 enum { WHT_FIRST = 0, WHT_FWD = 1, WHT_MID = 2, WHT_INV = 3, WHT_FINAL = 4 };
 
-constexpr int kWhtTile = 13;                          // tile bits of every pass
+constexpr int kWhtMinTile = 12;                       // tile bits of the passes: 12 or 13
+constexpr int kWhtMaxTile = 13;
 constexpr int kWhtMaxGroups = 4;                      // group 0 + up to 3 high groups
-constexpr int kWhtMaxOuter = DSE_MAX_HIGH_BITS(13);   // 21 outer bits at 34 qubits
+constexpr int kWhtMaxOuter = DSE_MAX_HIGH_BITS(12);   // 22 outer bits at 34 qubits
 constexpr int kWhtMaxQubits = 34;
 
 // Tile bit q of a group-g tile is global bit pos[q]; outer index bit i is global bit opos[i].
-// Group 0: pos = 0..12.  High groups: pos[0..c-1] = 0..c-1 (carried, not transformed in this
-// pass: contiguous 2^c-amplitude runs keep the loads coalesced), pos[c..12] = the group's bits.
+// Group 0: pos = 0..WL-1.  High groups: pos[0..c-1] = 0..c-1 (carried, not transformed in this
+// pass: contiguous 2^c-amplitude runs keep the loads coalesced), pos[c..WL-1] = the group's bits.
 struct WhtGroup {
-  int pos[kWhtTile];
+  int pos[kWhtMaxTile];
   int c;
   int n_outer;
   int opos[kWhtMaxOuter];
@@ -28,22 +29,23 @@ struct WhtProb {
   double2* vec_b;         // V-basis image of w (Y branch)
   const double* cquad;    // [n*n] symmetric: (pair_ij / 2) * 2^-n, zero diagonal
   // per-tile coefficient tables (launch_wht_tables), one row per outer index o:
-  double* ztab;           // [tiles][16] group 0: F_i(o) i < 13, C(o) without beta (D_Z, s = 1/2 - bit)
-  double* xytab;          // [tiles][32] MID group: F^X_q(o), C^X(o) at 0..13, F^Y, C^Y at 16..29
+  double* ztab;           // [tiles][16] group 0: F_i(o) i < WL, C(o) without beta (D_Z, s = 1/2 - bit)
+  double* xytab;          // [tiles][32] MID group: F^X_q(o), C^X(o) at 0..WL, F^Y, C^Y at 16..16+WL
   double lin_x[kWhtMaxQubits];  // Re c_1 of the drive of bit b, * 2^-n
   double lin_y[kWhtMaxQubits];  // Im c_1, * 2^-n
   int n;
+  int wl;                 // tile bits (== DevProb::L)
   int n_groups;
   WhtGroup grp[kWhtMaxGroups];
 };
 
 // Fills ztab / xytab of problem wp (device pointers to one WhtProb / DevProb entry).
-hipError_t launch_wht_tables(const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st);
+hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st);
 
 // One H application (mode MODE_APPLY) or one Chebyshev term (MODE_FIRST / MODE_GEN, buffer
 // roles and coefficient rows as launch_step) over items (problem, tile index): n_groups passes
-// FIRST, FWD x (G - 2), MID, INV x (G - 2), FINAL.  Every item's problem must have P.L == 13.
-hipError_t launch_wht_step(int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
+// FIRST, FWD x (G - 2), MID, INV x (G - 2), FINAL.  Every item's problem has P.L == wl.
+hipError_t launch_wht_step(int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
                            const int2* items, int n_items, int k, int q, int set, hipStream_t st);
 
 }  // namespace dse

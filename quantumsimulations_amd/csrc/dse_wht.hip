@@ -10,61 +10,74 @@
 // (reference: dipolar_ensemble_with_rare.py:516-560 builds the drive and flip-flop terms), applied
 // with ~n^2 diagonal work per amplitude instead of one partner-tile read per cross-tile term.
 //
-// The 2^n state lives in HBM; one H application is a few streaming passes over LDS tiles of 2^13
-// amplitudes.  Tile bits are split into groups (WhtGroup): group 0 = global bits 0..12, high
-// groups = up to 11 high bits each, completed to 13 tile bits by the lowest c "carried" global
-// bits.  The transform over all bits is the product of the groups' in-tile transforms:
+// The 2^n state lives in HBM; one H application is a few streaming passes over LDS tiles of 2^WL
+// amplitudes (WL = 12 or 13).  Tile bits are split into groups (WhtGroup): group 0 = global bits
+// 0..WL-1, high groups = up to WL-2 high bits each, completed to WL tile bits by the lowest c
+// "carried" global bits.  The transform over all bits is the product of the groups' transforms:
 //   FIRST  (group 0)          w -> A = W0 w,  B = W0 S^+ w            read 16, write 32 B/amp
 //   FWD    (groups 1..G-2)    A, B -> W_g A, W_g B                    read 32, write 32
 //   MID    (group G-1)        A -> W_g D_X W_g A,  B -> W_g D_Y W_g B  read 32, write 32
 //   INV    (groups G-2..1)    as FWD
 //   FINAL  (group 0)          out = D_Z w + W0 A + S W0 B, then the Chebyshev epilogue
-// G = 2 up to 24 qubits (three passes, ~200 B per amplitude and H application), G = 3 up to 35.
 //
-// In a tile, thread t of 512 owns 16 amplitudes; the 13 tile bits tau are spread over the thread
-// index and a register index differently in three layouts, and a layout change is one LDS
-// transpose (write, barrier, read).  Butterflies run on register bits, plus tile bit 0 (thread bit
-// 0 of layout C) across neighbouring lanes by DPP:
-//   A  r = tau[9..12]  t = tau[0..8]            (global loads and stores: coalesced)
-//   B  r = tau[5..8]   t = tau[0..4] | tau[9..12] << 5
-//   C  r = tau[1..4]   t = tau[0] | tau[5..12] << 1
-// LDS slot of tau: tau for A <-> B, tau + 2 (tau >> 5) for transposes to or from C -- both
-// conflict-free for ds_write_b128 (8-lane groups) and ds_read_b128 (16-lane groups) there, and
-// both additive in the register index (one base address per thread, immediate offsets per r).
+// In a tile, thread t of 2^(WL-4) owns 16 amplitudes; the tile bits tau are spread over a
+// register index r (4 bits at base b) and the thread index in three layouts,
+//   A  b = WL-4   (global loads)      B  b = WL-8   (global stores)      C  b = WL-12
+//   tau = (t & (2^b - 1)) | r << b | (t >> b) << (b + 4),
+// and a layout change is one LDS transpose (write, barrier, read).  Butterflies run on register
+// bits, plus tile bit 0 across neighbouring lanes by DPP in layout C when WL = 13.  A forward
+// transform visits A -> C -> B (skipping layouts without active bits) and stores from B, whose
+// lanes still cover runs of 16-32 consecutive amplitudes; MID comes back B -> C -> A.  LDS slots:
+// tau for A <-> B, tau + K (tau >> S) for transposes touching C (K, S = 2, 5 at WL = 13 and 1, 4
+// at WL = 12): conflict-free ds_write_b128 / ds_read_b128 except the C -> A read at WL = 12
+// (2-way), and separable, slot = f(t) + g(r): one base address per thread, immediate offsets.
+// WL = 12 tiles (64 KiB) fit two workgroups per CU, so one workgroup's loads overlap the other's
+// transposes; WL = 13 needs fewer passes below 25 qubits.
 #include "dse_device.h"
 #include "dse_wht.h"
 
 namespace dse {
 namespace {
 
-constexpr int WL = kWhtTile, WT = 1 << WL, WNT = 512, WR = 16;
+constexpr int WR = 16;
 
-__device__ __forceinline__ int tau_of(int lay, int r, int t) {
-  switch (lay) {
-    case 0: return (r << 9) | t;
-    case 1: return (t & 31) | (r << 5) | ((t >> 5) << 9);
-    default: return (t & 1) | (r << 1) | ((t >> 1) << 5);
-  }
+template <int WL>
+struct WG {
+  static constexpr int T = 1 << WL;
+  static constexpr int NT = 1 << (WL - 4);
+  static constexpr int LGNT = WL - 4;
+  static constexpr int PK = WL == 13 ? 2 : 1;  // slot pad of transposes touching layout C
+  static constexpr int PS = WL == 13 ? 5 : 4;
+  static constexpr int SLOTS = T + PK * ((T - 1) >> PS) + 1;
+};
+
+template <int WL>
+__host__ __device__ constexpr int rbase(int lay) { return WL - 4 - 4 * lay; }
+template <int WL>
+__host__ __device__ constexpr int tau_of(int lay, int r, int t) {
+  return (t & ((1 << rbase<WL>(lay)) - 1)) | (r << rbase<WL>(lay)) | ((t >> rbase<WL>(lay)) << (rbase<WL>(lay) + 4));
 }
-// tile bit of register bit i / thread bit j in a layout
-__device__ __forceinline__ int reg_tbit(int lay, int i) { return lay == 0 ? 9 + i : lay == 1 ? 5 + i : 1 + i; }
-__device__ __forceinline__ int thr_tbit(int lay, int j) {
-  switch (lay) {
-    case 0: return j;
-    case 1: return j < 5 ? j : 4 + j;
-    default: return j == 0 ? 0 : 4 + j;
-  }
-}
+template <int WL>
+__host__ __device__ constexpr int reg_tbit(int lay, int i) { return rbase<WL>(lay) + i; }
+template <int WL>
+__host__ __device__ constexpr int thr_tbit(int lay, int j) { return j < rbase<WL>(lay) ? j : j + 4; }
+template <int WL, bool PAD>
+__host__ __device__ constexpr int slot(int tau) { return PAD ? tau + WG<WL>::PK * (tau >> WG<WL>::PS) : tau; }
+
 // register mask of the bits a layout transforms in a group with c carried bits
+template <int WL>
 __device__ __forceinline__ int active_mask(int lay, int c) {
   int m = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (reg_tbit(lay, i) >= c) m |= 1 << i;
+    if (reg_tbit<WL>(lay, i) >= c) m |= 1 << i;
   return m;
 }
-// last layout of a forward sweep
-__device__ __forceinline__ int last_layout(int c) { return c <= 4 ? 2 : c <= 8 ? 1 : 0; }
+// layouts a forward transform visits after A: C holds bits rbase(2).., B bits rbase(1)..
+template <int WL>
+__device__ __forceinline__ bool has_c(int c) { return c < rbase<WL>(2) + 4; }
+template <int WL>
+__device__ __forceinline__ bool has_b(int c) { return c < rbase<WL>(1) + 4; }
 
 // butterflies (a + b, a - b) on the register bits in amask (wave-uniform)
 __device__ __forceinline__ void reg_wht(double2* v, int amask) {
@@ -89,7 +102,7 @@ __device__ __forceinline__ double lane_xor1(double x) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xB1, 0xF, 0xF, true);
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-// butterfly on thread bit 0 (tile bit 0 in layout C)
+// butterfly on thread bit 0 (tile bit 0 in layout C at WL = 13)
 __device__ __forceinline__ void lane0_wht(double2* v, int tid) {
   const double sg = (tid & 1) ? -1.0 : 1.0;
 #pragma unroll
@@ -100,120 +113,109 @@ __device__ __forceinline__ void lane0_wht(double2* v, int tid) {
   }
 }
 
-// LDS slot of (layout, r, t) = base(t) + stride * r (tau, or tau + 2 (tau >> 5) when padded)
-template <int LAY, bool PAD>
-__device__ __forceinline__ int slot_base(int t) {
-  if (LAY == 0) return PAD ? t + 2 * (t >> 5) : t;
-  if (LAY == 1) return (t & 31) + (t >> 5) * (PAD ? 544 : 512);
-  return (t & 1) + (t >> 1) * 34;  // C is always padded
-}
-template <int LAY, bool PAD>
-constexpr int slot_stride() { return LAY == 0 ? (PAD ? 544 : 512) : LAY == 1 ? (PAD ? 34 : 32) : 2; }
-
-template <int FROM, int TO>
+template <int WL, int FROM, int TO>
 __device__ __forceinline__ void transpose(double2* lds, double2* v, int tid) {
   constexpr bool PAD = FROM == 2 || TO == 2;
   __syncthreads();  // the previous transpose's reads are done
-  double2* wp = lds + slot_base<FROM, PAD>(tid);
+  double2* wp = lds + slot<WL, PAD>(tau_of<WL>(FROM, 0, tid));
 #pragma unroll
-  for (int r = 0; r < WR; ++r) wp[r * slot_stride<FROM, PAD>()] = v[r];
+  for (int r = 0; r < WR; ++r) wp[slot<WL, PAD>(tau_of<WL>(FROM, r, 0))] = v[r];
   __syncthreads();
-  const double2* rp = lds + slot_base<TO, PAD>(tid);
+  const double2* rp = lds + slot<WL, PAD>(tau_of<WL>(TO, 0, tid));
 #pragma unroll
-  for (int r = 0; r < WR; ++r) v[r] = rp[r * slot_stride<TO, PAD>()];
+  for (int r = 0; r < WR; ++r) v[r] = rp[slot<WL, PAD>(tau_of<WL>(TO, r, 0))];
 }
 
+template <int WL>
 __device__ __forceinline__ void layout_wht(double2* v, int lay, int c, int tid) {
-  reg_wht(v, active_mask(lay, c));
-  if (lay == 2 && c == 0) lane0_wht(v, tid);
+  reg_wht(v, active_mask<WL>(lay, c));
+  if (WL == 13 && lay == 2 && c == 0) lane0_wht(v, tid);
 }
-// forward sweep from layout A; returns the layout it ends in
+// forward transform of a group (c carried bits) from layout A; returns the layout it ends in
+template <int WL>
 __device__ __forceinline__ int tile_fwd(double2* lds, double2* v, int c, int tid) {
-  const int last = last_layout(c);
-  layout_wht(v, 0, c, tid);
-  if (last >= 1) {
-    transpose<0, 1>(lds, v, tid);
-    layout_wht(v, 1, c, tid);
+  layout_wht<WL>(v, 0, c, tid);
+  if (!has_b<WL>(c)) return 0;
+  if (has_c<WL>(c)) {
+    transpose<WL, 0, 2>(lds, v, tid);
+    layout_wht<WL>(v, 2, c, tid);
+    transpose<WL, 2, 1>(lds, v, tid);
+  } else {
+    transpose<WL, 0, 1>(lds, v, tid);
   }
-  if (last >= 2) {
-    transpose<1, 2>(lds, v, tid);
-    layout_wht(v, 2, c, tid);
-  }
-  return last;
+  layout_wht<WL>(v, 1, c, tid);
+  return 1;
 }
-// the same butterflies in reverse layout order, from layout `last` back to A
+// the same butterflies from layout `last` (tile_fwd's result) back to layout A
+template <int WL>
 __device__ __forceinline__ void tile_back(double2* lds, double2* v, int c, int last, int tid) {
-  if (last >= 2) {
-    layout_wht(v, 2, c, tid);
-    transpose<2, 1>(lds, v, tid);
+  if (last == 1) {
+    layout_wht<WL>(v, 1, c, tid);
+    if (has_c<WL>(c)) {
+      transpose<WL, 1, 2>(lds, v, tid);
+      layout_wht<WL>(v, 2, c, tid);
+      transpose<WL, 2, 0>(lds, v, tid);
+    } else {
+      transpose<WL, 1, 0>(lds, v, tid);
+    }
   }
-  if (last >= 1) {
-    layout_wht(v, 1, c, tid);
-    transpose<1, 0>(lds, v, tid);
-  }
-  layout_wht(v, 0, c, tid);
-}
-__device__ __forceinline__ void tile_full(double2* lds, double2* v, int c, int tid) {
-  const int last = tile_fwd(lds, v, c, tid);
-  if (last == 2) transpose<2, 0>(lds, v, tid);
-  if (last == 1) transpose<1, 0>(lds, v, tid);
+  layout_wht<WL>(v, 0, c, tid);
 }
 
+template <int WL>
 struct WhtShared {
-  double2 w[WT + 2 * (WT >> 5)];  // padded slots (slot_base)
-  double fx[WL + 1], fy[WL + 1];  // per-tile linear coefficients of D_X, D_Y (index WL: constant; xytab)
-  double cq[WL * WL];             // in-tile couplings c(q, q'), symmetric (D_X sign)
-  double zr[WR];                  // register-register part of D_X in the MID layout
-  double cz[WL + 1];              // D_Z of a group-0 tile: F_i(h), C(h) - beta (ztab)
+  double2 w[WG<WL>::SLOTS];
+  double f[2][WL + 1];  // MID: D_X, D_Y fields per tile bit + constant; FINAL: D_Z (z convention)
+  double cq[WL * WL];   // in-tile couplings (symmetric, z convention): MID pairs / FINAL zz / 4
+  double zr[WR];        // register-register part of the quadratic form in the diagonal's layout
 };
 
 __device__ __forceinline__ double zsign(uint64_t v, int b) { return ((v >> b) & 1ull) ? -1.0 : 1.0; }
 
-// In-tile couplings c(pos_q, pos_q') of a group (same for all its tiles).  No barrier.
-__device__ __forceinline__ void stage_couplings(const WhtProb& W, const WhtGroup& G, WhtShared& S, int tid) {
-  const gdbl* cq = gptr(W.cquad);
-  for (int e = tid; e < WL * WL; e += WNT) S.cq[e] = cq[G.pos[e / WL] * W.n + G.pos[e % WL]];
-}
-
 // zr[r] of layout lay (needs S.cq after a barrier)
-__device__ __forceinline__ void tile_zr(WhtShared& S, int lay, int tid) {
+template <int WL>
+__device__ __forceinline__ void tile_zr(WhtShared<WL>& S, int lay, int tid) {
   if (tid < WR) {
     double v = 0.0;
     for (int a = 0; a < 4; ++a)
       for (int b = a + 1; b < 4; ++b)
-        v += S.cq[reg_tbit(lay, a) * WL + reg_tbit(lay, b)] * (zsign(tid, a) * zsign(tid, b));
+        v += S.cq[reg_tbit<WL>(lay, a) * WL + reg_tbit<WL>(lay, b)] * (zsign(tid, a) * zsign(tid, b));
     S.zr[tid] = v;
   }
 }
 
-// v *= D_X (xsel) or D_Y in layout lay: per-thread part zt, register-bit fields hr, register
-// pairs zr (uniform per r).
-__device__ __forceinline__ void apply_xy_diag(const WhtShared& S, int lay, bool xsel, double2* v, int tid) {
-  const double sg = xsel ? 1.0 : -1.0;
-  const double* f = xsel ? S.fx : S.fy;
-  double zt = f[WL];
-  double hr[4];
+// Per-thread pieces of a quadratic form in layout lay (z_q = +-1 of tile bit q):
+//   linear  f[WL] + sum_q f[q] z_q          -> lt + sum_i lh[i] z_i(r)   (f = nullptr: none)
+//   pairs   sum_{q<q'} cq[q][q'] z_q z_q'   -> qt + sum_i qh[i] z_i(r) + zr[r]
+template <int WL>
+__device__ __forceinline__ void quad_parts(const double* f, const double* cq, int lay, int tid, double& lt,
+                                           double* lh, double& qt, double* qh) {
+  constexpr int LG = WG<WL>::LGNT;
+  lt = f[WL];
+  qt = 0.0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) hr[i] = f[reg_tbit(lay, i)];
-#pragma unroll 1
-  for (int j = 0; j < 9; ++j) {
-    const int qj = thr_tbit(lay, j);
+  for (int i = 0; i < 4; ++i) {
+    lh[i] = f[reg_tbit<WL>(lay, i)];
+    qh[i] = 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < LG; ++j) {
+    const int qj = thr_tbit<WL>(lay, j);
     const double zj = zsign(tid, j);
-    double a = f[qj];
-#pragma unroll 1
-    for (int i = j + 1; i < 9; ++i) a += sg * S.cq[qj * WL + thr_tbit(lay, i)] * zsign(tid, i);
-    zt += a * zj;
+    lt += f[qj] * zj;
+    double a = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) hr[i] += sg * S.cq[qj * WL + reg_tbit(lay, i)] * zj;
+    for (int i = j + 1; i < LG; ++i) a += cq[qj * WL + thr_tbit<WL>(lay, i)] * zsign(tid, i);
+    qt += a * zj;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qh[i] += cq[qj * WL + reg_tbit<WL>(lay, i)] * zj;
   }
+}
+__device__ __forceinline__ double quad_at(double zt, const double* hr, const double* zr, double sg, int r) {
+  double d = zt + sg * zr[r];
 #pragma unroll
-  for (int r = 0; r < WR; ++r) {
-    double d = zt + sg * S.zr[r];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) d += ((r >> i) & 1 ? -1.0 : 1.0) * hr[i];
-    v[r].x *= d;
-    v[r].y *= d;
-  }
+  for (int i = 0; i < 4; ++i) d += ((r >> i) & 1 ? -1.0 : 1.0) * hr[i];
+  return d;
 }
 
 // v * i^k
@@ -232,6 +234,36 @@ __device__ __forceinline__ uint64_t outer_bits(const WhtGroup& G, uint64_t o) {
   return x;
 }
 
+// global indices of this thread's amplitudes in layout lay: xo | xt | xr[r]
+template <int WL>
+struct LayIdx {
+  uint64_t xt;
+  uint64_t xr[WR];
+  __device__ __forceinline__ LayIdx(const WhtGroup& G, int lay, int tid, uint64_t xo) {
+    xt = xo;
+    for (int j = 0; j < WG<WL>::LGNT; ++j) xt |= (uint64_t)((tid >> j) & 1) << G.pos[thr_tbit<WL>(lay, j)];
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      uint64_t a = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a |= (uint64_t)((r >> i) & 1) << G.pos[reg_tbit<WL>(lay, i)];
+      xr[r] = a;
+    }
+  }
+  __device__ __forceinline__ uint64_t operator[](int r) const { return xt | xr[r]; }
+};
+
+// group 0 (pos = identity): global index = o << WL | tau, the register part an immediate
+template <int WL>
+struct LayIdx0 {
+  uint64_t xt;
+  int lay;
+  __device__ __forceinline__ LayIdx0(int lay_, int tid, uint64_t o) : lay(lay_) {
+    xt = (o << WL) | (uint64_t)tau_of<WL>(lay, 0, tid);
+  }
+  __device__ __forceinline__ uint64_t operator[](int r) const { return xt | (uint64_t)tau_of<WL>(lay, r, 0); }
+};
+
 // input vector of term k (buffer roles of k_step_rb)
 __device__ __forceinline__ int win_role(int mode, int k, int q) {
   if (mode == MODE_APPLY) return 0;
@@ -239,11 +271,11 @@ __device__ __forceinline__ int win_role(int mode, int k, int q) {
   return ((k - 1) & 1) ? 1 : (q ? 2 : 0);
 }
 
-template <int PASS, int MODE>
-__global__ void __launch_bounds__(WNT)
+template <int WL, int PASS, int MODE>
+__global__ void __launch_bounds__(WG<WL>::NT)
 k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, const int2* __restrict__ items,
       int g, int k, int q, int set) {
-  __shared__ WhtShared S;
+  __shared__ WhtShared<WL> S;
   const int2 it = items[blockIdx.x];
   const WhtProb& W = probs[it.x];
   const DevProb& P = dprobs[it.x];
@@ -252,101 +284,150 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   const WhtGroup& G = W.grp[g];
   const uint64_t o = (uint64_t)(uint32_t)it.y;  // outer index of the tile
   const uint64_t xo = outer_bits(G, o);
-
-  // global indices of this thread's amplitudes in layout A: xo | xt | xr[r]
-  uint64_t xt = 0;
-  for (int j = 0; j < 9; ++j) xt |= (uint64_t)((tid >> j) & 1) << G.pos[j];
-  uint64_t xr[WR];
-#pragma unroll
-  for (int r = 0; r < WR; ++r) {
-    uint64_t a = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a |= (uint64_t)((r >> i) & 1) << G.pos[9 + i];
-    xr[r] = a;
-  }
-  const uint64_t xb = xo | xt;
-
   double2 v[WR];
   if (PASS == WHT_FIRST) {
+    const LayIdx0<WL> ia(0, tid, o);
     const gd2* win = gptr((const double2*)P.buf[win_role(MODE, k, q)]);
     double2 u[WR];
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-      v[r] = gld(win, xb | xr[r]);
-      u[r] = mul_ipow(v[r], -__popcll(xb | xr[r]));  // S^+ of every qubit
+      v[r] = gld(win, ia[r]);
+      u[r] = mul_ipow(v[r], -__popcll(ia[r]));  // S^+ of every qubit
     }
-    tile_full(S.w, v, 0, tid);
+    tile_fwd<WL>(S.w, v, 0, tid);  // ends in layout B
+    const LayIdx0<WL> is(1, tid, o);
     gd2* A = gptr(W.vec_a);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) gst(A, xb | xr[r], v[r]);
-    tile_full(S.w, u, 0, tid);
+    for (int r = 0; r < WR; ++r) gst(A, is[r], v[r]);
+    tile_fwd<WL>(S.w, u, 0, tid);
     gd2* B = gptr(W.vec_b);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) gst(B, xb | xr[r], u[r]);
+    for (int r = 0; r < WR; ++r) gst(B, is[r], u[r]);
     return;
   }
 
-  if (PASS == WHT_FWD || PASS == WHT_INV || PASS == WHT_MID) {
-    const int lm = last_layout(G.c);
-    if (PASS == WHT_MID) {
-      stage_couplings(W, G, S, tid);
-      if (tid < 32) {
-        const double c = gptr((const double*)W.xytab)[o * 32 + tid];
-        if (tid <= WL) S.fx[tid] = c;
-        else if (tid >= 16 && tid <= 16 + WL) S.fy[tid - 16] = c;
-      }
-      __syncthreads();
-      tile_zr(S, lm, tid);  // read after the first transpose's barriers
-    }
+  const LayIdx<WL> ia(G, 0, tid, xo);  // loads of the FWD / INV / MID passes
+  if (PASS == WHT_FWD || PASS == WHT_INV) {
+    const int last = has_b<WL>(G.c) ? 1 : 0;
+    const LayIdx<WL> is(G, last, tid, xo);
 #pragma unroll 1
     for (int vec = 0; vec < 2; ++vec) {
       gd2* X = gptr(vec == 0 ? W.vec_a : W.vec_b);
 #pragma unroll
-      for (int r = 0; r < WR; ++r) v[r] = gld(X, xb | xr[r]);
-      if (PASS == WHT_MID) {
-        if (lm == 0) __syncthreads();  // no transpose before the diagonal: S.zr
-        tile_fwd(S.w, v, G.c, tid);
-        apply_xy_diag(S, lm, vec == 0, v, tid);
-        tile_back(S.w, v, G.c, lm, tid);
-      } else {
-        tile_full(S.w, v, G.c, tid);
-      }
+      for (int r = 0; r < WR; ++r) v[r] = gld(X, ia[r]);
+      tile_fwd<WL>(S.w, v, G.c, tid);
 #pragma unroll
-      for (int r = 0; r < WR; ++r) gst(X, xb | xr[r], v[r]);
+      for (int r = 0; r < WR; ++r) gst(X, is[r], v[r]);
+    }
+    return;
+  }
+
+  if (PASS == WHT_MID) {
+    const int last = has_b<WL>(G.c) ? 1 : 0;
+    {
+      const gd2* XA = gptr((const double2*)W.vec_a);  // in flight under the staging
+#pragma unroll
+      for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+    }
+    {
+      const gdbl* cq = gptr(W.cquad);
+      for (int e = tid; e < WL * WL; e += WG<WL>::NT) S.cq[e] = cq[G.pos[e / WL] * W.n + G.pos[e % WL]];
+      if (tid < 32) {
+        const double c = gptr((const double*)W.xytab)[o * 32 + tid];
+        if (tid <= WL) S.f[0][tid] = c;
+        else if (tid >= 16 && tid <= 16 + WL) S.f[1][tid - 16] = c;
+      }
+      __syncthreads();
+      tile_zr<WL>(S, last, tid);
+    }
+    // D_X = lin_X + Q, D_Y = lin_Y - Q (Q: the pair form, shared)
+    double xt, xh[4], yt, yh[4], qt, qh[4];
+    quad_parts<WL>(S.f[0], S.cq, last, tid, xt, xh, qt, qh);
+    {
+      double q2, qh2[4];
+      quad_parts<WL>(S.f[1], S.cq, last, tid, yt, yh, q2, qh2);
+    }
+    __syncthreads();  // S.zr
+#pragma unroll 1
+    for (int vec = 0; vec < 2; ++vec) {
+      gd2* X = gptr(vec == 0 ? W.vec_a : W.vec_b);
+      if (vec == 1) {
+#pragma unroll
+        for (int r = 0; r < WR; ++r) v[r] = gld(X, ia[r]);
+      }
+      tile_fwd<WL>(S.w, v, G.c, tid);
+      {
+        const double sg = vec == 0 ? 1.0 : -1.0;
+        double h[4];
+        const double t0 = (vec == 0 ? xt : yt) + sg * qt;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = (vec == 0 ? xh[i] : yh[i]) + sg * qh[i];
+#pragma unroll
+        for (int r = 0; r < WR; ++r) {
+          const double d = quad_at(t0, h, S.zr, sg, r);
+          v[r].x *= d;
+          v[r].y *= d;
+        }
+      }
+      tile_back<WL>(S.w, v, G.c, last, tid);
+#pragma unroll
+      for (int r = 0; r < WR; ++r) gst(X, ia[r], v[r]);
     }
     return;
   }
 
   // ---- FINAL (group 0 tile = ordinary tile h): out = D_Z w + W0 A + S W0 B, then the recurrence
   if (PASS == WHT_FINAL) {
-    const uint32_t h = (uint32_t)o;
-    if (tid <= WL) {
-      const double c = gptr((const double*)W.ztab)[(uint64_t)h * 16 + tid];
-      S.cz[tid] = (tid == WL && MODE != MODE_APPLY) ? c - P.beta : c;
+    constexpr int last = 1;  // group 0 ends every forward transform in layout B
+    const LayIdx0<WL> ia0(0, tid, o);
+    // D_Z in the z convention: fields F_i / 2, constant C(h) - beta, in-tile zz / 4
+    {
+      if (tid <= WL) {
+        const double c = gptr((const double*)W.ztab)[o * 16 + tid];
+        S.f[0][tid] = tid == WL ? (MODE == MODE_APPLY ? c : c - P.beta) : 0.5 * c;
+      }
+      const gdbl* zz = gptr(P.zz);
+      for (int e = tid; e < WL * WL; e += WG<WL>::NT) {
+        const int a = e / WL, b = e % WL;
+        S.cq[e] = a == b ? 0.0 : 0.25 * (a < b ? zz[a * P.n + b] : zz[b * P.n + a]);
+      }
+      __syncthreads();
+      tile_zr<WL>(S, last, tid);
     }
     double2 out[WR];
-    const gd2* B = gptr((const double2*)W.vec_b);
+    {
+      const gd2* B = gptr((const double2*)W.vec_b);
+      const gd2* A = gptr((const double2*)W.vec_a);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) out[r] = gld(B, xb | xr[r]);
-    tile_full(S.w, out, 0, tid);
+      for (int r = 0; r < WR; ++r) out[r] = gld(B, ia0[r]);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) out[r] = mul_ipow(out[r], __popcll(xb | xr[r]));  // S of every qubit
-    const gd2* A = gptr((const double2*)W.vec_a);
-#pragma unroll
-    for (int r = 0; r < WR; ++r) v[r] = gld(A, xb | xr[r]);
-    tile_full(S.w, v, 0, tid);
+      for (int r = 0; r < WR; ++r) v[r] = gld(A, ia0[r]);
+    }
+    tile_fwd<WL>(S.w, out, 0, tid);
+    tile_fwd<WL>(S.w, v, 0, tid);
+    const LayIdx0<WL> is(last, tid, o);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-      out[r].x += v[r].x;
-      out[r].y += v[r].y;
+      const double2 s = mul_ipow(out[r], __popcll(is[r]));  // S of every qubit
+      out[r].x = s.x + v[r].x;
+      out[r].y = s.y + v[r].y;
     }
-    __syncthreads();  // S.cz
-    // D_Z(x) = zzlo[x_lo] + C(h) + sum_i F_i(h) s_i(x_lo),  s = 1/2 - bit,  x_lo = r * 512 + tid
-    double gt = S.cz[WL];
+    // D_Z(x) = zt + sum_i hr[i] z_i(r) + zr[r] (linear and pair parts summed, outer loop rolled)
+    double zt = S.f[0][WL], hr[4];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) gt += S.cz[i] * (0.5 - (double)((tid >> i) & 1));
+    for (int i = 0; i < 4; ++i) hr[i] = S.f[0][reg_tbit<WL>(last, i)];
+#pragma unroll 1
+    for (int j = 0; j < WG<WL>::LGNT; ++j) {
+      const int qj = thr_tbit<WL>(last, j);
+      const double zj = zsign(tid, j);
+      double a = S.f[0][qj];
+#pragma unroll 1
+      for (int i = j + 1; i < WG<WL>::LGNT; ++i) a += S.cq[qj * WL + thr_tbit<WL>(last, i)] * zsign(tid, i);
+      zt += a * zj;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hr[i] += S.cq[qj * WL + reg_tbit<WL>(last, i)] * zj;
+    }
     const gd2* win = gptr((const double2*)P.buf[win_role(MODE, k, q)]);
-    const gdbl* zzlo = gptr(P.zzlo);
     gd2* psi_b = gptr(P.buf[q ? 2 : 0]);
     gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
     gd2* scr_b = gptr(P.buf[1]);
@@ -356,13 +437,11 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     const double scale = MODE == MODE_GEN ? 2.0 * P.s1 : P.s1;
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-      const double2 own = gld(win, xb | xr[r]);
-      double d = zzlo[r * WNT + tid] + gt;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) d += S.cz[9 + i] * (((r >> i) & 1) ? -0.5 : 0.5);
+      const double2 own = gld(win, is[r]);
+      const double d = quad_at(zt, hr, S.zr, 1.0, r);
       out[r].x = fma(d, own.x, out[r].x);
       out[r].y = fma(d, own.y, out[r].y);
-      step_epilogue<MODE>(xb | xr[r], out[r], own, scale, wdst, acc_b, C, 0);
+      step_epilogue<MODE>(is[r], out[r], own, scale, wdst, acc_b, C, 0);
     }
   }
 }
@@ -370,6 +449,7 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
 // One thread per tile o: D_Z pieces of group-0 tile o (tile_diag_coeffs without beta) and the
 // D_X / D_Y pieces of MID-group tile o:  F_q = lin(pos_q) + sum_i c(pos_q, opos_i) z_i,
 // C = sum_i lin(opos_i) z_i + sum_{i<j} c(opos_i, opos_j) z_i z_j  (D_Y: lin_y, -c).
+template <int WL>
 __global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ wp, const DevProb* __restrict__ dp,
                                                     int64_t tiles) {
   const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -390,20 +470,20 @@ __global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ 
     for (int i = WL; i < j; ++i) c += P.zz[i * n + j] * ((0.5 - (double)((o >> (i - WL)) & 1)) * sj);
   }
   zt[WL] = c;
-  zt[WL + 1] = zt[WL + 2] = 0.0;
+  for (int i = WL + 1; i < 16; ++i) zt[i] = 0.0;
   const WhtGroup& G = W.grp[W.n_groups - 1];
   const double* cq = W.cquad;
   double* xy = W.xytab + o * 32;
-  for (int q = 0; q < WL; ++q) {
-    const int b = G.pos[q];
+  for (int qb = 0; qb < WL; ++qb) {
+    const int b = G.pos[qb];
     double fx = W.lin_x[b], fy = W.lin_y[b];
     for (int i = 0; i < G.n_outer; ++i) {
       const double v = cq[b * n + G.opos[i]] * zsign(o, i);
       fx += v;
       fy -= v;
     }
-    xy[q] = fx;
-    xy[16 + q] = fy;
+    xy[qb] = fx;
+    xy[16 + qb] = fy;
   }
   double cx = 0.0, cy = 0.0;
   for (int i = 0; i < G.n_outer; ++i) {
@@ -419,41 +499,55 @@ __global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ 
   }
   xy[WL] = cx;
   xy[16 + WL] = cy;
-  xy[14] = xy[15] = xy[30] = xy[31] = 0.0;
+  for (int i = WL + 1; i < 16; ++i) xy[i] = xy[16 + i] = 0.0;
 }
 
-template <int PASS>
+template <int WL, int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
                        int g, int k, int q, int set, hipStream_t st) {
-  const dim3 grid(n_items), block(WNT);
+  const dim3 grid(n_items), block(WG<WL>::NT);
   if (mode == MODE_APPLY)
-    hipLaunchKernelGGL((k_wht<PASS, MODE_APPLY>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_APPLY>), grid, block, 0, st, wp, dp, items, g, k, q, set);
   else if (mode == MODE_FIRST)
-    hipLaunchKernelGGL((k_wht<PASS, MODE_FIRST>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_FIRST>), grid, block, 0, st, wp, dp, items, g, k, q, set);
   else
-    hipLaunchKernelGGL((k_wht<PASS, MODE_GEN>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_GEN>), grid, block, 0, st, wp, dp, items, g, k, q, set);
   return hipGetLastError();
+}
+
+template <int WL>
+hipError_t wht_step(int mode, int n_groups, const WhtProb* wp, const DevProb* dp, const int2* items,
+                    int n_items, int k, int q, int set, hipStream_t st) {
+  hipError_t e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+  for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
+    e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, st);
+  if (e == hipSuccess) e = launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, st);
+  for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
+    e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, st);
+  if (e == hipSuccess) e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+  return e;
 }
 
 }  // namespace
 
-hipError_t launch_wht_tables(const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st) {
-  hipLaunchKernelGGL(k_wht_tables, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, st, wp, dp, tiles);
+hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st) {
+  const dim3 grid((unsigned)((tiles + 255) / 256)), block(256);
+  if (wl == 12)
+    hipLaunchKernelGGL(k_wht_tables<12>, grid, block, 0, st, wp, dp, tiles);
+  else if (wl == 13)
+    hipLaunchKernelGGL(k_wht_tables<13>, grid, block, 0, st, wp, dp, tiles);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-hipError_t launch_wht_step(int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
+hipError_t launch_wht_step(int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
                            const int2* items, int n_items, int k, int q, int set, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   if (n_groups < 2 || n_groups > kWhtMaxGroups) return hipErrorInvalidValue;
-  hipError_t e = launch_pass<WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, st);
-  for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
-    e = launch_pass<WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, st);
-  if (e == hipSuccess) e = launch_pass<WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, st);
-  for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
-    e = launch_pass<WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, st);
-  if (e == hipSuccess) e = launch_pass<WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, st);
-  return e;
+  if (wl == 12) return wht_step<12>(mode, n_groups, wp, dp, items, n_items, k, q, set, st);
+  if (wl == 13) return wht_step<13>(mode, n_groups, wp, dp, items, n_items, k, q, set, st);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace dse

@@ -26,25 +26,29 @@ def _apply(engine, prob, v, **opts):
         return engine.apply_h(pid, v)
     finally:
         engine.set_option("wht", 1)
-        engine.set_option("wht_group_bits", 11)
+        engine.set_option("wht_group_bits", 0)
+        engine.set_option("wht_tile_bits", 0)
 
 
-# n, group bits -> high groups of sizes (carried bits c = 13 - size)
-@pytest.mark.parametrize("n,gbits", [(14, 11), (15, 11), (17, 11), (17, 2), (20, 11), (20, 4),
-                                     (20, 3), (19, 9)])
-def test_wht_apply_matches_oracle(engine, n, gbits):
+# n, group bits, tile bits -> high groups of sizes s (carried bits c = tile bits - s): every pass
+# count G = 2..4 and every layout sequence (A; A, B; A, C, B) of both tile sizes
+@pytest.mark.parametrize("n,gbits,wl", [(15, 11, 13), (17, 11, 13), (17, 2, 13), (20, 11, 13),
+                                        (20, 4, 13), (20, 3, 13), (19, 9, 13), (21, 9, 13),
+                                        (14, 0, 12), (15, 0, 12), (17, 2, 12), (20, 0, 12),
+                                        (20, 3, 12), (21, 0, 12), (18, 6, 12)])
+def test_wht_apply_matches_oracle(engine, n, gbits, wl):
     prob = _random_problem(n, 700 + n + gbits)
     v = _rand(n, 7 + n)
-    out = _apply(engine, prob, v, wht=1, wht_group_bits=gbits)
+    out = _apply(engine, prob, v, wht=1, wht_group_bits=gbits, wht_tile_bits=wl)
     ref = rm.bitwise_apply(_tables(prob), v)
     assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
 
 
-@pytest.mark.parametrize("n", [22, 24])
-def test_wht_apply_matches_step_kernels(engine, n):
+@pytest.mark.parametrize("n,wl", [(22, 13), (24, 13), (22, 12), (24, 12)])
+def test_wht_apply_matches_step_kernels(engine, n, wl):
     prob = _random_problem(n, 900 + n)
     v = _rand(n, 11 + n)
-    a = _apply(engine, prob, v, wht=1)
+    a = _apply(engine, prob, v, wht=1, wht_tile_bits=wl)
     b = _apply(engine, prob, v, wht=0)
     assert np.max(np.abs(a - b)) <= 1e-13 * np.max(np.abs(b))
 
@@ -60,7 +64,8 @@ def test_wht_sweep_problem_imaginary_drive(engine):
     assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
 
 
-def test_wht_evolve_matches_step_kernels_and_expm(engine):
+@pytest.mark.parametrize("wl", [13, 12])
+def test_wht_evolve_matches_step_kernels_and_expm(engine, wl):
     import scipy.sparse as sp
     from scipy.sparse.linalg import expm_multiply
     from quantumsimulations_amd.dipolar_ensemble_with_rare import problem_to_csr
@@ -73,6 +78,7 @@ def test_wht_evolve_matches_step_kernels_and_expm(engine):
         for wht in (0, 1):
             engine.clear()
             engine.set_option("wht", wht)
+            engine.set_option("wht_tile_bits", wl)
             for p in probs:
                 engine.add(p)
             res[wht], st = engine.evolve(t)
@@ -80,6 +86,7 @@ def test_wht_evolve_matches_step_kernels_and_expm(engine):
             states[wht] = [engine.state(i) for i in range(len(probs))]
     finally:
         engine.set_option("wht", 1)
+        engine.set_option("wht_tile_bits", 0)
     np.testing.assert_allclose(res[1], res[0], rtol=0, atol=1e-11)
     psi0 = np.zeros(1 << n, dtype=complex)
     psi0[probs[2].psi0_index] = 1.0
@@ -91,7 +98,7 @@ def test_wht_not_used_for_small_tiles_or_persistent(engine):
     prob = _random_problem(16, 5)
     t = np.linspace(0.0, 1e-4, 3)
     engine.clear()
-    engine.set_option("tile_bits", 12)
+    engine.set_option("tile_bits", 11)
     try:
         engine.add(prob)
         _, st = engine.evolve(t)
