@@ -62,7 +62,7 @@ struct HostProblem {
   double2* rbuf_own[kMaxShards] = {};  // dist: receive buffers of the exchange, per mask
   bool imag = false;         // every drive coefficient purely imaginary (drive phase pi/2)
   // Walsh-Hadamard engine (dse_wht.hip): X- and Y-branch vectors and the pair matrix
-  double2* wvec[2] = {nullptr, nullptr};
+  double2* wvec[4] = {nullptr, nullptr, nullptr, nullptr};  // A, B (+ index-swapped A, B)
   double* d_cquad = nullptr;
   double* d_wtab = nullptr;  // ztab | xytab
   int wht_groups = 0;        // passes' tile-bit groups; 0: this problem uses the step kernels
@@ -73,6 +73,7 @@ struct LaneGroup {
   int L = 0;
   int tiles = 1;            // tiles per problem (persistent mode: 1 or 2)
   int wht_groups = 0;       // > 0: every problem of the group runs on the Walsh-Hadamard engine
+  std::vector<std::pair<int, int>> wht_regs;  // partitioned registers: (first shard, degree)
   int64_t off = 0;          // first position in the global item array
   int64_t count = 0;        // items of this group
   std::vector<int> active;     // active[k] = items with degree >= k (prefix of the group)
@@ -214,7 +215,7 @@ int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
   const int nl = p.n_local;   // qubits held in this context (n unless partitioned)
   int L = std::max(std::min(nl, ctx->tile_bits), std::max(kMinTile, nl - 32));
   // registers for the Walsh-Hadamard engine (whole, more than two 2^13 tiles) take its tile size
-  if (ctx->wht && ctx->tile_bits == kMaxTile && p.shard_bits == 0 && nl > kMaxTile + 1)
+  if (ctx->wht && ctx->tile_bits == kMaxTile && nl > kMaxTile + 1)
     L = ctx->wht_tile_bits ? ctx->wht_tile_bits : (nl <= 24 ? 13 : 12);
   if (L > kMaxTile) return fail(ctx, DSE_ERR_ARG, "problem too large for the tile range");
   p.L = L;
@@ -436,37 +437,70 @@ int prepare(dse_ctx* ctx) {
 }
 
 // ---- Walsh-Hadamard engine ------------------------------------------------------------------
-// Tile-bit groups of an n-qubit register (WhtGroup): group 0 = bits 0..12; the n - 13 high bits
-// in ceil((n - 13) / max_bits) contiguous, balanced groups, each completed by carried low bits.
-int wht_layout(int n, int wl, int max_bits, WhtProb& w) {
-  const int h = n - wl;
-  if (h < 1 || h > kWhtMaxOuter) return 0;
-  const int ng = (h + max_bits - 1) / max_bits;
-  if (ng + 1 > kWhtMaxGroups) return 0;
-  WhtGroup& g0 = w.grp[0];
-  for (int q = 0; q < wl; ++q) g0.pos[q] = q;
-  g0.c = 0;
-  g0.n_outer = h;
-  for (int i = 0; i < h; ++i) g0.opos[i] = wl + i;
-  int first = wl;
-  for (int gi = 0; gi < ng; ++gi) {
-    const int s = h / ng + (gi < h % ng ? 1 : 0);
-    WhtGroup& g = w.grp[gi + 1];
-    g.c = wl - s;
-    std::vector<int> in(n, 0);
-    for (int q = 0; q < g.c; ++q) g.pos[q] = q, in[q] = 1;
-    for (int i = 0; i < s; ++i) g.pos[g.c + i] = first + i, in[first + i] = 1;
-    int o = 0;
-    for (int b = 0; b < n; ++b)
-      if (!in[b]) g.opos[o++] = b;
-    g.n_outer = o;
-    first += s;
-  }
-  return ng + 1;
+// WhtGroup of the given high bits: completed to wl tile bits by the lowest carried bits; every
+// other local bit is an outer bit.
+WhtGroup make_group(const std::vector<int>& bits, int wl, int n_local) {
+  WhtGroup g;
+  std::memset(&g, 0, sizeof(g));
+  const int s = (int)bits.size();
+  g.c = wl - s;
+  std::vector<int> in(n_local, 0);
+  for (int q = 0; q < g.c; ++q) g.pos[q] = q, in[q] = 1;
+  for (int i = 0; i < s; ++i) g.pos[g.c + i] = bits[i], in[bits[i]] = 1;
+  int o = 0;
+  for (int b = 0; b < n_local; ++b)
+    if (!in[b]) g.opos[o++] = b;
+  g.n_outer = o;
+  return g;
 }
 
-// Builds the engine's tables and vectors for the problems it can take: whole registers (not
-// sharded) of more than one 2^13 tile.  Idempotent until free_device.
+// balanced split of bits into ceil(|bits| / max_bits) contiguous groups
+std::vector<std::vector<int>> split_bits(const std::vector<int>& bits, int max_bits) {
+  std::vector<std::vector<int>> out;
+  const int h = (int)bits.size();
+  if (h == 0) return out;
+  const int ng = (h + max_bits - 1) / max_bits;
+  int first = 0;
+  for (int gi = 0; gi < ng; ++gi) {
+    const int s = h / ng + (gi < h % ng ? 1 : 0);
+    out.emplace_back(bits.begin() + first, bits.begin() + first + s);
+    first += s;
+  }
+  return out;
+}
+
+// Tile-bit groups of a register of n_local local qubits (w.grp, returns G; 0: not possible).
+// Group 0 = local bits 0..wl-1.  Unpartitioned: the high bits in balanced groups of <= max_bits,
+// the last one is MID's.  Partitioned (S shard bits): the pre-swap groups must transform the top
+// S local bits T (they leave with the index swap); MID transforms the shard bits that arrive in
+// T's positions together with up to max_bits - S other local high bits.
+int wht_layout(int n_local, int S, int wl, int max_bits, WhtProb& w) {
+  const int h = n_local - wl;
+  if (h < 1 || h > kWhtMaxOuter || h < S || max_bits <= S) return 0;
+  std::vector<int> high;
+  for (int b = wl; b < n_local; ++b) high.push_back(b);
+  std::vector<std::vector<int>> groups;
+  if (S == 0) {
+    groups = split_bits(high, max_bits);
+  } else {
+    const std::vector<int> rest(high.begin(), high.end() - S), T(high.end() - S, high.end());
+    const int m = std::min(max_bits - S, (int)rest.size());
+    std::vector<int> mid(rest.begin(), rest.begin() + m), pre(rest.begin() + m, rest.end());
+    pre.insert(pre.end(), T.begin(), T.end());
+    groups = split_bits(pre, max_bits);
+    mid.insert(mid.end(), T.begin(), T.end());
+    groups.push_back(mid);
+  }
+  if ((int)groups.size() + 1 > kWhtMaxGroups) return 0;
+  w.grp[0] = make_group({}, wl, n_local);  // pos = 0..wl-1, outer = the high bits
+  w.grp[0].c = 0;                           // group 0 transforms all its tile bits
+  for (size_t gi = 0; gi < groups.size(); ++gi) w.grp[gi + 1] = make_group(groups[gi], wl, n_local);
+  return (int)groups.size() + 1;
+}
+
+// Builds the engine's tables and vectors for the problems it can take: registers of more than one
+// tile, whole or partitioned (loopback shards or one shard per process).  Idempotent until
+// free_device.
 int ensure_wht(dse_ctx* ctx) {
   if (ctx->wht_ready) return DSE_OK;
   std::vector<WhtProb> hw(ctx->probs.size());
@@ -474,11 +508,11 @@ int ensure_wht(dse_ctx* ctx) {
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     HostProblem& p = ctx->probs[pi];
     p.wht_groups = 0;
-    if (!ctx->wht || p.L < kWhtMinTile || p.L > kWhtMaxTile || p.n_tiles < 2 || p.shard_bits > 0) continue;
-    const int n = p.n;
+    if (!ctx->wht || p.L < kWhtMinTile || p.L > kWhtMaxTile || p.n_tiles < 2) continue;
+    const int n = p.n, nl = p.n_local, S = p.shard_bits;
     WhtProb& w = hw[pi];
     const int gb = ctx->wht_group_bits ? std::min(ctx->wht_group_bits, p.L - 2) : p.L - 2;
-    const int G = wht_layout(n, p.L, gb, w);
+    const int G = wht_layout(nl, S, p.L, gb, w);
     if (G < 2) continue;
     const double sc = std::ldexp(1.0, -n);
     std::vector<double> cq(size_t(n) * n, 0.0);
@@ -490,20 +524,32 @@ int ensure_wht(dse_ctx* ctx) {
       w.lin_x[b] = re * sc;
       w.lin_y[b] = im * sc;
     }
-    const size_t vbytes = (size_t(1) << n) * sizeof(double2);
-    if (hipMalloc(&p.wvec[0], vbytes) != hipSuccess || hipMalloc(&p.wvec[1], vbytes) != hipSuccess ||
-        hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) != hipSuccess ||
-        hipMalloc(&p.d_wtab, (size_t)p.n_tiles * 48 * sizeof(double)) != hipSuccess)
+    const size_t vbytes = (size_t(1) << nl) * sizeof(double2);
+    const int nvec = S > 0 ? 4 : 2;
+    bool ok = hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) == hipSuccess &&
+              hipMalloc(&p.d_wtab, (size_t)p.n_tiles * 48 * sizeof(double)) == hipSuccess;
+    for (int v = 0; v < nvec && ok; ++v) ok = hipMalloc(&p.wvec[v], vbytes) == hipSuccess;
+    if (!ok)
       return fail(ctx, DSE_ERR_OOM, "device allocation of the Walsh-Hadamard vectors failed (" +
-                                        std::to_string(2 * vbytes) + " bytes per problem; option wht = 0 "
+                                        std::to_string(nvec * vbytes) + " bytes per problem; option wht = 0 "
                                         "uses the step kernels)");
     HIPC(hipMemcpy(p.d_cquad, cq.data(), cq.size() * sizeof(double), hipMemcpyHostToDevice));
     w.vec_a = p.wvec[0];
     w.vec_b = p.wvec[1];
+    w.vec_at = S > 0 ? p.wvec[2] : p.wvec[0];
+    w.vec_bt = S > 0 ? p.wvec[3] : p.wvec[1];
+    for (int b = 0; b < n; ++b) w.gmap[b] = b;
+    if (S > 0) {  // MID state: local bits nl-S+i hold global nl+i, the rank holds global nl-S+i
+      for (int i = 0; i < S; ++i) w.gmap[nl - S + i] = nl + i;
+      w.fix_mask = ((uint64_t(1) << S) - 1) << (nl - S);
+      w.fix_val = (uint64_t)p.shard_rank << (nl - S);
+      w.phase0 = __builtin_popcount((unsigned)p.shard_rank);
+    }
     w.cquad = p.d_cquad;
     w.ztab = p.d_wtab;
     w.xytab = p.d_wtab + (size_t)p.n_tiles * 16;
     w.n = n;
+    w.n_local = nl;
     w.wl = p.L;
     w.n_groups = G;
     p.wht_groups = G;
@@ -516,6 +562,51 @@ int ensure_wht(dse_ctx* ctx) {
       HIPC(launch_wht_tables(ctx->probs[pi].L, ctx->d_wht + pi, ctx->d_probs + pi, ctx->probs[pi].n_tiles, ctx->lanes[0].stream));
   HIPC(hipStreamSynchronize(ctx->lanes[0].stream));
   ctx->wht_ready = true;
+  return DSE_OK;
+}
+
+// Index swap of the X/Y vectors of partitioned registers (local top S bits <-> shard bits):
+// chunk p of shard r -> chunk r of shard p; an involution, so back = the same exchange from the
+// swapped copies.  Loopback registers: device copies; one shard per process: RCCL all-to-all.
+int wht_swap(dse_ctx* ctx, const std::vector<int>& regs, bool back, hipStream_t st) {
+  for (int first : regs) {
+    const HostProblem& P0 = ctx->probs[first];
+    const int S = P0.shard_bits;
+    const size_t chunk = size_t(1) << (P0.n_local - S);
+    const size_t cbytes = chunk * sizeof(double2);
+    for (int v = 0; v < 2; ++v) {
+      if (P0.dist) {
+        const double2* src = P0.wvec[back ? 2 + v : v];
+        double2* dst = P0.wvec[back ? v : 2 + v];
+        const ncclResult_t r = ncclAllToAll(src, dst, cbytes, ncclUint8, ctx->comm, st);
+        if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+        continue;
+      }
+      for (int r = 0; r < (1 << S); ++r)
+        for (int p = 0; p < (1 << S); ++p) {
+          const HostProblem& Pr = ctx->probs[first + r];
+          const HostProblem& Pp = ctx->probs[first + p];
+          const double2* src = (back ? Pr.wvec[2 + v] : Pr.wvec[v]) + p * chunk;
+          double2* dst = (back ? Pp.wvec[v] : Pp.wvec[2 + v]) + r * chunk;
+          HIPC(hipMemcpyAsync(dst, src, cbytes, hipMemcpyDeviceToDevice, st));
+        }
+    }
+  }
+  return DSE_OK;
+}
+
+// One WHT application (mode / term k) over items of problems with wht_groups == G, tile wl;
+// regs: first problem of every partitioned register among them (index swaps around MID).
+// segs: (items, count) launches of the same wl / G.
+int wht_run(dse_ctx* ctx, int wl, int G, const std::vector<std::pair<const int2*, int>>& segs,
+            const std::vector<int>& regs, int mode, int k, int q, int set, hipStream_t st) {
+  int rc;
+  for (int part = WHT_PART_PRE; part <= WHT_PART_POST; ++part) {
+    if (part == WHT_PART_MID && !regs.empty() && (rc = wht_swap(ctx, regs, false, st))) return rc;
+    if (part == WHT_PART_POST && !regs.empty() && (rc = wht_swap(ctx, regs, true, st))) return rc;
+    for (const auto& sg : segs)
+      HIPC(launch_wht_part(part, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, st));
+  }
   return DSE_OK;
 }
 
@@ -925,14 +1016,20 @@ int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out
     const size_t amps = size_t(1) << P.n_local;
     HIPC(hipMemcpyAsync(P.buf[0], in + i * amps, amps * sizeof(double2), hipMemcpyHostToDevice, st));
   }
-  if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
   if ((rc = ensure_wht(ctx))) return rc;
-  for (int i = 0; i < count; ++i) {
-    HostProblem& P = ctx->probs[first + i];
-    if (P.wht_groups)
-      HIPC(launch_wht_step(P.L, MODE_APPLY, P.wht_groups, ctx->d_wht, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
-    else
+  if (ctx->probs[first].wht_groups) {  // all members alike
+    const HostProblem& P0 = ctx->probs[first];
+    std::vector<std::pair<const int2*, int>> segs;
+    for (int i = 0; i < count; ++i) segs.push_back({ctx->probs[first + i].d_items, (int)ctx->probs[first + i].n_tiles});
+    std::vector<int> regs;
+    if (P0.shard_bits > 0) regs.push_back(first);
+    if ((rc = wht_run(ctx, P0.L, P0.wht_groups, segs, regs, MODE_APPLY, 0, 0, 0, st))) return rc;
+  } else {
+    if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
+    for (int i = 0; i < count; ++i) {
+      HostProblem& P = ctx->probs[first + i];
       HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+    }
   }
   for (int i = 0; i < count; ++i) {
     HostProblem& P = ctx->probs[first + i];
@@ -1016,9 +1113,14 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   }
   // streaming: registers of more than one 2^13 tile take the Walsh-Hadamard engine (option wht)
   bool used_wht = false;
+  bool any_dist_step = any_dist;  // dist shards on the step kernels: per-term shard exchange
   if (!persistent) {
     if ((rc = ensure_wht(ctx))) return rc;
-    for (auto& P : ctx->probs) used_wht = used_wht || P.wht_groups > 0;
+    any_dist_step = false;
+    for (auto& P : ctx->probs) {
+      used_wht = used_wht || P.wht_groups > 0;
+      any_dist_step = any_dist_step || (P.dist && P.wht_groups == 0);
+    }
   }
   // Outputs per launch M: the Chebyshev series of e^{-iH tau} converges after ~ alpha tau +
   // O((alpha tau)^{1/3}) terms, so M outputs from one series (one propagator sum per output, same
@@ -1215,6 +1317,14 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       g.wht_groups = persistent ? 0 : ctx->probs[kv.second.front()].wht_groups;
       for (int pi : kv.second)
         if (ctx->probs[pi].wht_groups != g.wht_groups) g.wht_groups = 0;
+      g.wht_regs.clear();
+      if (g.wht_groups)
+        for (int pi : kv.second) {
+          const HostProblem& P = ctx->probs[pi];
+          if (P.shard_bits == 0) continue;
+          const int first = P.dist ? pi : P.group_first;
+          if (P.dist || P.shard_rank == 0) g.wht_regs.push_back({first, P.degree});
+        }
       const int gdeg = ctx->probs[kv.second.front()].degree;
       g.active.assign(gdeg + 2, 0);
       g.bytes.assign(gdeg + 2, 0.0);
@@ -1371,27 +1481,32 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
           }
           continue;
         }
-        if (any_dist && (rc = dist_exchange(ctx, q ? 2 : 0, 1, ln.stream))) return rc;
-        auto step = [&](int mode, int na, int k) {
-          return g.wht_groups ? launch_wht_step(g.L, mode, g.wht_groups, ctx->d_wht, ctx->d_probs, ctx->d_items + g.off,
-                                                na, k, q, set, ln.stream)
-                              : launch_step(g.L, mode, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream);
+        if (any_dist_step && (rc = dist_exchange(ctx, q ? 2 : 0, 1, ln.stream))) return rc;
+        auto step = [&](int mode, int na, int k) -> int {
+          if (g.wht_groups) {
+            std::vector<int> regs;
+            for (const auto& rg : g.wht_regs)
+              if (rg.second >= k) regs.push_back(rg.first);
+            return wht_run(ctx, g.L, g.wht_groups, {{ctx->d_items + g.off, na}}, regs, mode, k, q, set, ln.stream);
+          }
+          HIPC(launch_step(g.L, mode, ctx->d_probs, ctx->d_items + g.off, na, k, q, set, ln.stream));
+          return DSE_OK;
         };
-        HIPC(step(MODE_FIRST, g.active[1], 1));
+        if ((rc = step(MODE_FIRST, g.active[1], 1))) return rc;
         for (int k = 2; k < (int)g.active.size(); ++k) {
           const int na = g.active[k];
           if (na <= 0) break;
-          if (any_dist && (rc = dist_exchange(ctx, ((k - 1) & 1) ? 1 : (q ? 2 : 0), k, ln.stream)))
+          if (any_dist_step && (rc = dist_exchange(ctx, ((k - 1) & 1) ? 1 : (q ? 2 : 0), k, ln.stream)))
             return rc;
           if (timed) {
             const size_t i = ln.ev_used[pool]++;
             HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
-            HIPC(step(MODE_GEN, na, k));
+            if ((rc = step(MODE_GEN, na, k))) return rc;
             HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
             pool_bytes[li * 2 + pool].push_back(g.flops[k]);
             pool_bytes2[li * 2 + pool].push_back(g.bytes[k]);
           } else {
-            HIPC(step(MODE_GEN, na, k));
+            if ((rc = step(MODE_GEN, na, k))) return rc;
           }
           launches += 1.0;
           amp_updates += (double)na * T;

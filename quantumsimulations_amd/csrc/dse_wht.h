@@ -27,13 +27,23 @@ struct WhtGroup {
 struct WhtProb {
   double2* vec_a;         // W-basis image of w (X branch)
   double2* vec_b;         // V-basis image of w (Y branch)
+  // Partitioned register (shard r of 2^S, local bits n_local = n - S): the MID pass runs on the
+  // index-swapped copies (vec_at, vec_bt: local top S bits <-> shard bits, an all-to-all between
+  // the shards); gmap[local bit] = global bit in that state, the global bits then held by the
+  // rank index are fix_mask with values fix_val.  Unpartitioned: vec_*t = vec_*, gmap = identity.
+  double2* vec_at;
+  double2* vec_bt;
+  uint64_t fix_mask, fix_val;
+  int gmap[kWhtMaxQubits];
+  int phase0;             // popcount of the rank's global bits (S phases of FIRST / FINAL)
   const double* cquad;    // [n*n] symmetric: (pair_ij / 2) * 2^-n, zero diagonal
   // per-tile coefficient tables (launch_wht_tables), one row per outer index o:
   double* ztab;           // [tiles][16] group 0: F_i(o) i < WL, C(o) without beta (D_Z, s = 1/2 - bit)
   double* xytab;          // [tiles][32] MID group: F^X_q(o), C^X(o) at 0..WL, F^Y, C^Y at 16..16+WL
   double lin_x[kWhtMaxQubits];  // Re c_1 of the drive of bit b, * 2^-n
   double lin_y[kWhtMaxQubits];  // Im c_1, * 2^-n
-  int n;
+  int n;                  // qubits of the whole register
+  int n_local;            // qubits held in this context (n - S)
   int wl;                 // tile bits (== DevProb::L)
   int n_groups;
   WhtGroup grp[kWhtMaxGroups];
@@ -43,9 +53,12 @@ struct WhtProb {
 hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st);
 
 // One H application (mode MODE_APPLY) or one Chebyshev term (MODE_FIRST / MODE_GEN, buffer
-// roles and coefficient rows as launch_step) over items (problem, tile index): n_groups passes
-// FIRST, FWD x (G - 2), MID, INV x (G - 2), FINAL.  Every item's problem has P.L == wl.
-hipError_t launch_wht_step(int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
+// roles and coefficient rows as launch_step) over items (problem, tile index), in three parts:
+//   pre  = FIRST, FWD over groups 1..G-2      mid = MID (group G-1)      post = INV, FINAL
+// (partitioned registers swap vec_* <-> vec_*t between the parts).  Every item's problem has
+// P.L == wl.
+enum { WHT_PART_PRE = 0, WHT_PART_MID = 1, WHT_PART_POST = 2 };
+hipError_t launch_wht_part(int part, int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
                            const int2* items, int n_items, int k, int q, int set, hipStream_t st);
 
 }  // namespace dse

@@ -292,7 +292,7 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       v[r] = gld(win, ia[r]);
-      u[r] = mul_ipow(v[r], -__popcll(ia[r]));  // S^+ of every qubit
+      u[r] = mul_ipow(v[r], -(__popcll(ia[r]) + W.phase0));  // S^+ of every qubit
     }
     tile_fwd<WL>(S.w, v, 0, tid);  // ends in layout B
     const LayIdx0<WL> is(1, tid, o);
@@ -325,13 +325,14 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   if (PASS == WHT_MID) {
     const int last = has_b<WL>(G.c) ? 1 : 0;
     {
-      const gd2* XA = gptr((const double2*)W.vec_a);  // in flight under the staging
+      const gd2* XA = gptr((const double2*)W.vec_at);  // in flight under the staging
 #pragma unroll
       for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
     }
     {
       const gdbl* cq = gptr(W.cquad);
-      for (int e = tid; e < WL * WL; e += WG<WL>::NT) S.cq[e] = cq[G.pos[e / WL] * W.n + G.pos[e % WL]];
+      for (int e = tid; e < WL * WL; e += WG<WL>::NT)
+        S.cq[e] = cq[W.gmap[G.pos[e / WL]] * W.n + W.gmap[G.pos[e % WL]]];
       if (tid < 32) {
         const double c = gptr((const double*)W.xytab)[o * 32 + tid];
         if (tid <= WL) S.f[0][tid] = c;
@@ -350,7 +351,7 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     __syncthreads();  // S.zr
 #pragma unroll 1
     for (int vec = 0; vec < 2; ++vec) {
-      gd2* X = gptr(vec == 0 ? W.vec_a : W.vec_b);
+      gd2* X = gptr(vec == 0 ? W.vec_at : W.vec_bt);
       if (vec == 1) {
 #pragma unroll
         for (int r = 0; r < WR; ++r) v[r] = gld(X, ia[r]);
@@ -408,7 +409,7 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     const LayIdx0<WL> is(last, tid, o);
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
-      const double2 s = mul_ipow(out[r], __popcll(is[r]));  // S of every qubit
+      const double2 s = mul_ipow(out[r], __popcll(is[r]) + W.phase0);  // S of every qubit
       out[r].x = s.x + v[r].x;
       out[r].y = s.y + v[r].y;
     }
@@ -457,28 +458,43 @@ __global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ 
   const WhtProb& W = *wp;
   const DevProb& P = *dp;
   const int n = W.n;
+  // D_Z: global tile index (a shard's rank bits above its local tiles)
+  const uint64_t hg = (uint64_t)P.h_base | (uint64_t)o;
   double* zt = W.ztab + o * 16;
   for (int i = 0; i < WL; ++i) {
     double f = P.field[i];
-    for (int j = WL; j < n; ++j) f += P.zz[i * n + j] * (0.5 - (double)((o >> (j - WL)) & 1));
+    for (int j = WL; j < n; ++j) f += P.zz[i * n + j] * (0.5 - (double)((hg >> (j - WL)) & 1));
     zt[i] = f;
   }
   double c = P.shift;
   for (int j = WL; j < n; ++j) {
-    const double sj = 0.5 - (double)((o >> (j - WL)) & 1);
+    const double sj = 0.5 - (double)((hg >> (j - WL)) & 1);
     c += P.field[j] * sj;
-    for (int i = WL; i < j; ++i) c += P.zz[i * n + j] * ((0.5 - (double)((o >> (i - WL)) & 1)) * sj);
+    for (int i = WL; i < j; ++i) c += P.zz[i * n + j] * ((0.5 - (double)((hg >> (i - WL)) & 1)) * sj);
   }
   zt[WL] = c;
   for (int i = WL + 1; i < 16; ++i) zt[i] = 0.0;
+  // D_X / D_Y of the MID group: outer bits (through gmap) and the rank-held bits are "outer"
   const WhtGroup& G = W.grp[W.n_groups - 1];
   const double* cq = W.cquad;
+  int ob[kWhtMaxQubits];
+  double oz[kWhtMaxQubits];
+  int no = 0;
+  for (int i = 0; i < G.n_outer; ++i) {
+    ob[no] = W.gmap[G.opos[i]];
+    oz[no++] = zsign(o, i);
+  }
+  for (int b = 0; b < n; ++b)
+    if ((W.fix_mask >> b) & 1ull) {
+      ob[no] = b;
+      oz[no++] = zsign(W.fix_val, b);
+    }
   double* xy = W.xytab + o * 32;
   for (int qb = 0; qb < WL; ++qb) {
-    const int b = G.pos[qb];
+    const int b = W.gmap[G.pos[qb]];
     double fx = W.lin_x[b], fy = W.lin_y[b];
-    for (int i = 0; i < G.n_outer; ++i) {
-      const double v = cq[b * n + G.opos[i]] * zsign(o, i);
+    for (int i = 0; i < no; ++i) {
+      const double v = cq[b * n + ob[i]] * oz[i];
       fx += v;
       fy -= v;
     }
@@ -486,13 +502,11 @@ __global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ 
     xy[16 + qb] = fy;
   }
   double cx = 0.0, cy = 0.0;
-  for (int i = 0; i < G.n_outer; ++i) {
-    const int bi = G.opos[i];
-    const double zi = zsign(o, i);
-    cx += W.lin_x[bi] * zi;
-    cy += W.lin_y[bi] * zi;
-    for (int j = i + 1; j < G.n_outer; ++j) {
-      const double v = cq[bi * n + G.opos[j]] * (zi * zsign(o, j));
+  for (int i = 0; i < no; ++i) {
+    cx += W.lin_x[ob[i]] * oz[i];
+    cy += W.lin_y[ob[i]] * oz[i];
+    for (int j = i + 1; j < no; ++j) {
+      const double v = cq[ob[i] * n + ob[j]] * (oz[i] * oz[j]);
       cx += v;
       cy -= v;
     }
@@ -516,15 +530,20 @@ hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int
 }
 
 template <int WL>
-hipError_t wht_step(int mode, int n_groups, const WhtProb* wp, const DevProb* dp, const int2* items,
+hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const DevProb* dp, const int2* items,
                     int n_items, int k, int q, int set, hipStream_t st) {
-  hipError_t e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, st);
-  for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
-    e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, st);
-  if (e == hipSuccess) e = launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, st);
-  for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
-    e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, st);
-  if (e == hipSuccess) e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+  hipError_t e = hipSuccess;
+  if (part == WHT_PART_PRE) {
+    e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+    for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
+      e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, st);
+  } else if (part == WHT_PART_MID) {
+    e = launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, st);
+  } else {
+    for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
+      e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, st);
+    if (e == hipSuccess) e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+  }
   return e;
 }
 
@@ -541,12 +560,12 @@ hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64
   return hipGetLastError();
 }
 
-hipError_t launch_wht_step(int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
+hipError_t launch_wht_part(int part, int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
                            const int2* items, int n_items, int k, int q, int set, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   if (n_groups < 2 || n_groups > kWhtMaxGroups) return hipErrorInvalidValue;
-  if (wl == 12) return wht_step<12>(mode, n_groups, wp, dp, items, n_items, k, q, set, st);
-  if (wl == 13) return wht_step<13>(mode, n_groups, wp, dp, items, n_items, k, q, set, st);
+  if (wl == 12) return wht_part<12>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, st);
+  if (wl == 13) return wht_part<13>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, st);
   return hipErrorInvalidValue;
 }
 

@@ -120,3 +120,44 @@ def test_wht_evolve_is_bitwise_deterministic(engine):
     runs = [engine.evolve(t)[0] for _ in range(2)]
     assert np.array_equal(runs[0], runs[1])
     assert np.array_equal(engine.state(0), engine.state(0))
+
+
+# partitioned registers (loopback shards on one GPU): the index swap (all-to-all of the X / Y
+# vectors between shards) around MID, the rank-held bits of the MID diagonal and the rank phase
+@pytest.mark.parametrize("n,bits,wl,gbits", [(16, 1, 13, 0), (17, 2, 13, 0), (19, 3, 13, 0),
+                                             (18, 3, 12, 0), (20, 2, 12, 0), (20, 3, 13, 0),
+                                             (22, 3, 12, 4)])
+def test_wht_sharded_apply_matches_oracle(engine, n, bits, wl, gbits):
+    prob = _random_problem(n, 1500 + n + bits, rare_bit=n - 1)
+    v = _rand(n, 3 * n + bits)
+    engine.clear()
+    engine.set_option("wht_tile_bits", wl)
+    engine.set_option("wht_group_bits", gbits)
+    try:
+        ps = engine.add_sharded(prob, bits)
+        out = engine.apply_h(ps, v)
+    finally:
+        engine.clear()
+        engine.set_option("wht_tile_bits", 0)
+        engine.set_option("wht_group_bits", 0)
+    ref = rm.bitwise_apply(_tables(prob), v)
+    assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("n,bits", [(17, 2), (19, 3)])
+def test_wht_sharded_evolve_matches_unsharded(engine, n, bits):
+    prob = _random_problem(n, 1700 + n, rare_bit=n - 1)
+    t = np.linspace(0.0, 2e-4, 4)
+    engine.clear()
+    p0 = engine.add(prob)
+    ref, st0 = engine.evolve(t)
+    s_ref = engine.state(p0)
+    engine.clear()
+    ps = engine.add_sharded(prob, bits)
+    obs, st = engine.evolve(t)
+    s_sh = engine.state(ps)
+    engine.clear()
+    assert st0["mode"] == 2 and st["mode"] == 2
+    for i in range(1 << bits):
+        np.testing.assert_allclose(obs[ps + i], ref[p0], rtol=0, atol=1e-12)
+    assert np.max(np.abs(s_sh - s_ref)) < 1e-12
