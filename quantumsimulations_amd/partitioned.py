@@ -1,12 +1,14 @@
 """One register partitioned over GPUs (SURVEY.md §8(e), configs with N >= 28).
 
 The top ``shard_bits`` engine qubits are global: rank r of 2^shard_bits (one process per GPU)
-holds the amplitudes whose global bits equal r.  In engine order the rare spin is the top qubit,
-so it is always global; its only off-diagonal term is its own drive flip (sea-rare coupling is
-ZZ only, dipolar_ensemble_with_rare.py:562-568), so the global set {rare, s1, s2} needs partner
-masks {rare, s1, s2, s1^s2}: at most 4 full-shard exchanges per H application (RCCL
-send/recv pairs inside libdse, include/dse.h dse_add_problem_sharded), and one all-reduce of
-the observable sums at the end.
+holds the amplitudes whose global bits equal r.  On the Walsh-Hadamard engine (default) every H
+application index-swaps the X / Y vectors around its MID pass (local top bits <-> shard bits: an
+RCCL all-to-all inside libdse, twice per vector).  On the step kernels (option wht = 0): in
+engine order the rare spin is the top qubit, so it is always global; its only off-diagonal term
+is its own drive flip (sea-rare coupling is ZZ only, dipolar_ensemble_with_rare.py:562-568), so
+the global set {rare, s1, s2} needs partner masks {rare, s1, s2, s1^s2}: at most 4 full-shard
+exchanges per term (RCCL send/recv pairs, include/dse.h dse_add_problem_sharded).  Either way
+one all-reduce of the observable sums at the end.
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_partitioned.py
 

@@ -5,9 +5,11 @@
     python tools/bench_partitioned.py --loopback 8        # all 8 shards on one GPU (test mode)
 
 Rank r holds shard r of the N = n_sea + 1 qubit center_on register (top log2(world) qubits
-global, the rare spin among them); every Chebyshev term exchanges whole shards with the partner
-ranks the terms couple (RCCL send/recv, include/dse.h).  Rank 0 prints one JSON line: ms per H
-application, exchanged bytes per H application and rank, the observables at t_final.
+global, the rare spin among them).  Walsh-Hadamard engine (default, --wht 1): every H application
+index-swaps the X / Y vectors twice (RCCL all-to-all, 4 shard-sized transfers of which 1/world
+stays local); step kernels (--wht 0): every term exchanges whole shards with the partner ranks the
+terms couple (RCCL send/recv).  Rank 0 prints one JSON line: ms per H application, exchanged
+bytes per H application and rank, the observables at t_final.
 """
 from __future__ import annotations
 
@@ -35,6 +37,7 @@ def main():
     ap.add_argument("--steps", type=int, default=11)
     ap.add_argument("--delta", type=float, default=50e3)
     ap.add_argument("--loopback", type=int, default=0, help="all shards on one GPU (2, 4 or 8)")
+    ap.add_argument("--wht", type=int, default=1)
     a = ap.parse_args()
     p = sweep_point_params(a.n_sea, a.delta, "center_on", a.t_final, a.steps)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -44,6 +47,7 @@ def main():
     if a.loopback:
         bits = shard_bits_for(a.loopback)
         with Engine(0) as eng:
+            eng.set_option("wht", a.wht)
             pid = eng.add_sharded(prob, bits)
             t0 = time.perf_counter()
             obs, st = eng.evolve(np.linspace(0.0, a.t_final, a.steps))
@@ -57,6 +61,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("gloo")       # bootstrap only; the data path is RCCL in libdse
         with Engine(local) as eng:
+            eng.set_option("wht", a.wht)
             join(eng, rank, world, dist)
             dist.barrier()
             t0 = time.perf_counter()
@@ -82,14 +87,17 @@ def main():
         elif len(gbits) == 2:
             n_masks += int(prob.pair[min(gbits), max(gbits)] != 0)
     shard_bytes = (1 << (n - bits)) * 16
+    wht = st.get("mode") == 2
+    xbytes = 4 * shard_bytes * (shards - 1) // shards if wht else n_masks * shard_bytes
     if rank == 0:
         print(json.dumps({
             "config": f"config 5: N={n} center_on delta={a.delta:g} Hz, t_final={a.t_final}, "
                       f"{a.steps} outputs, {shards} shards ({mode})",
             "wall_s": wall, "h_applications": st["h_applications"],
             "ms_per_h_application": wall / max(st["h_applications"], 1) * 1e3,
-            "shard_GiB": shard_bytes / 2**30, "partner_masks": n_masks,
-            "exchange_bytes_per_h_per_rank": n_masks * shard_bytes,
+            "shard_GiB": shard_bytes / 2**30, "engine_mode": st.get("mode"),
+            "exchange": "index-swap all-to-all of A, B (x2)" if wht else f"send/recv, {n_masks} partner masks",
+            "exchange_bytes_per_h_per_rank": xbytes,
             "obs_t_final": obs_d,
         }), flush=True)
 
