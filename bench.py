@@ -218,7 +218,9 @@ def main():
     else:
         achieved = k_bytes / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
         roof = {
-            "kernel": "k_step_rb<13,MODE_GEN> (Chebyshev step: H|w>, recurrence, accumulation)",
+            "kernel": ("k_wht passes (Walsh-Hadamard engine: one Chebyshev term = FIRST, MID, FINAL)"
+                       if mode == 2 else
+                       "k_step_rb<13,MODE_GEN> (Chebyshev step: H|w>, recurrence, accumulation)"),
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
             "algorithmic_bytes_per_amp": 58.7,
@@ -249,7 +251,7 @@ def main():
             "global_points_per_step": len(my_det) * world,
             "evolutions_per_step_per_gpu": len(probs),
             "propagator": "exact Chebyshev (tol 1e-14)",
-            "engine_mode": "persistent" if mode == 1 else "streaming",
+            "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(mode, "streaming"),
             "tile_bits": args.tile_bits,
             "streams": args.streams,
             "outputs_per_launch": stats[-1].get("outputs_per_launch"),

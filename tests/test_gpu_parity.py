@@ -252,7 +252,7 @@ def test_persistent_matches_streaming_and_expm(engine, n, tile_bits):
             for p in probs:
                 engine.add(p)
             res[pers], st = engine.evolve(t)
-            assert st["mode"] == (1 if pers else (2 if tile_bits == 13 and n > 13 else 0))
+            assert st["mode"] == (1 if pers else (2 if tile_bits >= 12 and n > tile_bits else 0))
             states[pers] = [engine.state(i) for i in range(len(probs))]
     finally:
         engine.set_option("persistent", 1)
