@@ -16,7 +16,9 @@ rank, no data-path collective (evolutions are independent).
 Extra fields: "roofline" (dominant kernel: the Chebyshev step, HIP events around
 each launch inside the timed region) and "cpu_baseline" (rank 0, N = 1 only: the
 QuTiP-5 sesolve equivalent -- scipy ZVODE-Adams + CSR, oracle/propagate.py --
-on a bounded sample, extrapolated linearly in simulated time).
+on a bounded sample, extrapolated linearly in simulated time) and "large_register"
+(rank 0, N = 1 only: config 5 on one GPU, N = 24, the Walsh-Hadamard engine's passes
+against the HBM roofline; --no-large skips it).
 """
 from __future__ import annotations
 
@@ -55,6 +57,7 @@ def parse():
                     help="persistent mode: output times propagated per launch from one Chebyshev series")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
     ap.add_argument("--n-det", type=int, default=N_DET)
+    ap.add_argument("--no-large", action="store_true", help="skip the config-5 single-GPU leg")
     return ap.parse_args()
 
 
@@ -106,6 +109,40 @@ def cpu_baseline(budget_s: float):
                    f"{[round(r * 1e6, 1) for r in reached]} us of the {T_FINAL * 1e6:.0f} us grid, "
                    f"extrapolated linearly in simulated time; 1 core"),
         "seconds_per_point_extrapolated": total_wall_full,
+    }
+
+
+def large_register(device: int, n_sea: int = 23):
+    """Config 5 on one GPU (N = n_sea + 1, center_on, 50 kHz, t_final 1e-5 s, 11 outputs): the
+    Walsh-Hadamard engine's H|psi> passes against the HBM roofline.  Bytes per amplitude and H
+    application are the passes' algorithmic traffic (FIRST 48, FWD/MID/INV 64 each, FINAL 80 + acc
+    32 every third term), equal to the rocprofv3 FETCH/WRITE counts (profiles/r01/wht_n24_pmc_traffic.json)."""
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.engine import Engine
+    from quantumsimulations_amd.sweep import sweep_point_params
+    p = sweep_point_params(n_sea, 50e3, "center_on", 1e-5, 11)
+    prob = pb.build_problem(p)
+    n = prob.n_qubits
+    wl = 13 if n <= 24 else 12
+    groups = 1 + -(-(n - wl) // (wl - 2))
+    bpa = 48.0 + 64.0 * (2 * groups - 3) + 80.0 + 32.0 / 3.0
+    with Engine(device) as eng:
+        eng.add(prob)
+        t = np.linspace(0.0, 1e-5, 11)
+        eng.evolve(t)                                    # warm-up (tables, code objects)
+        t0 = time.perf_counter()
+        _, st = eng.evolve(t)
+        wall = time.perf_counter() - t0
+    per_term_ms = st["step_kernel_ms"] / max(st["timed_launches"], 1)
+    gbs = bpa * (1 << n) / (per_term_ms * 1e-3) / 1e9
+    return {
+        "workload": f"config 5 on one GPU: N={n} center_on, 50 kHz, t_final 1e-5 s, 11 outputs",
+        "engine_mode": st["mode"], "tile_bits": wl, "passes_per_h": 2 * groups - 1,
+        "ms_per_h_application": wall / st["h_applications"] * 1e3,
+        "kernel_ms_per_h_application": per_term_ms,
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa,
+                     "traffic_source": "profiles/r01/wht_n24_pmc_traffic.json"},
     }
 
 
@@ -200,7 +237,8 @@ def main():
         traffic, traffic_src = pmc_traffic("k_interval<13, true>") if args.tile_bits == 13 else (None, None)
         roof = {
             "kernel": "k_interval<13> (persistent Chebyshev interval: all K terms on chip)",
-            "bound": "fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "compute": "FP64 VALU (MI355X: FP64 vector peak = dense FP64 MFMA peak = 78.6 TF/s)",
             "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
             "traffic_source": traffic_src,
             "traffic_rate_gbs": (traffic / (k_ms / k_launches * 1e-3) / 1e9) if (traffic and k_launches) else None,
@@ -266,9 +304,14 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
         except Exception as exc:  # report, never hide
             line["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    eng.close()
+    if rank == 0 and world == 1 and not args.no_large:
+        try:
+            line["large_register"] = large_register(local)
+        except Exception as exc:  # report, never hide
+            line["large_register"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(line), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
