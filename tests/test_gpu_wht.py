@@ -144,19 +144,23 @@ def test_wht_sharded_apply_matches_oracle(engine, n, bits, wl, gbits):
     assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
 
 
-@pytest.mark.parametrize("n,bits", [(17, 2), (19, 3)])
-def test_wht_sharded_evolve_matches_unsharded(engine, n, bits):
+@pytest.mark.parametrize("n,bits,wl", [(17, 2, 13), (19, 3, 13), (18, 2, 12), (19, 3, 12)])
+def test_wht_sharded_evolve_matches_unsharded(engine, n, bits, wl):
     prob = _random_problem(n, 1700 + n, rare_bit=n - 1)
     t = np.linspace(0.0, 2e-4, 4)
     engine.clear()
-    p0 = engine.add(prob)
-    ref, st0 = engine.evolve(t)
-    s_ref = engine.state(p0)
-    engine.clear()
-    ps = engine.add_sharded(prob, bits)
-    obs, st = engine.evolve(t)
-    s_sh = engine.state(ps)
-    engine.clear()
+    engine.set_option("wht_tile_bits", wl)
+    try:
+        p0 = engine.add(prob)
+        ref, st0 = engine.evolve(t)
+        s_ref = engine.state(p0)
+        engine.clear()
+        ps = engine.add_sharded(prob, bits)
+        obs, st = engine.evolve(t)
+        s_sh = engine.state(ps)
+    finally:
+        engine.clear()
+        engine.set_option("wht_tile_bits", 0)
     assert st0["mode"] == 2 and st["mode"] == 2
     for i in range(1 << bits):
         np.testing.assert_allclose(obs[ps + i], ref[p0], rtol=0, atol=1e-12)
