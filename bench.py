@@ -123,7 +123,7 @@ def large_register(device: int, n_sea: int = 23):
     p = sweep_point_params(n_sea, 50e3, "center_on", 1e-5, 11)
     prob = pb.build_problem(p)
     n = prob.n_qubits
-    wl = 13 if n <= 24 else 12
+    wl = 13
     groups = 1 + -(-(n - wl) // (wl - 2))
     bpa = 48.0 + 64.0 * (2 * groups - 3) + 80.0 + 32.0 / 3.0
     with Engine(device) as eng:

@@ -117,8 +117,8 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "wht"          1 (default): streaming registers of more than one tile (n >= 14,
  *                         not sharded) apply H as D_Z + W D_X W + V D_Y V^+ (Walsh-Hadamard
  *                         passes, two extra state-sized vectors per problem); 0: step kernels
- *          "wht_tile_bits"   tile of that engine: 12, 13, or 0 (default: 13 up to 24 qubits,
- *                         else 12, two workgroups per CU)
+ *          "wht_tile_bits"   tile of that engine: 12 (two workgroups per CU), 13, or 0 (default:
+ *                         13)
  *          "wht_group_bits"  high qubits transformed per pass of that engine, 2..11, or 0
  *                         (default: tile bits - 2)
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with

@@ -112,7 +112,7 @@ struct dse_ctx {
   int persistent = 1;               // use k_interval when every problem fits <= 2 tiles
   int wht = 1;                      // Walsh-Hadamard engine for registers of more tiles
   int wht_group_bits = 0;           // high bits per pass of that engine (0: tile bits - 2)
-  int wht_tile_bits = 0;            // its tile: 12, 13, 0 = 13 up to 24 qubits, else 12
+  int wht_tile_bits = 0;            // its tile: 12, 13 (0 = 13)
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
@@ -216,7 +216,7 @@ int build_tables(dse_ctx* ctx, HostProblem& p, DevProb& d) {
   int L = std::max(std::min(nl, ctx->tile_bits), std::max(kMinTile, nl - 32));
   // registers for the Walsh-Hadamard engine (whole, more than two 2^13 tiles) take its tile size
   if (ctx->wht && ctx->tile_bits == kMaxTile && nl > kMaxTile + 1)
-    L = ctx->wht_tile_bits ? ctx->wht_tile_bits : (nl <= 24 ? 13 : 12);
+    L = ctx->wht_tile_bits ? ctx->wht_tile_bits : 13;
   if (L > kMaxTile) return fail(ctx, DSE_ERR_ARG, "problem too large for the tile range");
   p.L = L;
   p.n_tiles = int64_t(1) << (nl - L);

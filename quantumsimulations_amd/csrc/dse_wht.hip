@@ -310,15 +310,20 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   if (PASS == WHT_FWD || PASS == WHT_INV) {
     const int last = has_b<WL>(G.c) ? 1 : 0;
     const LayIdx<WL> is(G, last, tid, xo);
-#pragma unroll 1
-    for (int vec = 0; vec < 2; ++vec) {
-      gd2* X = gptr(vec == 0 ? W.vec_a : W.vec_b);
+    // both vectors' loads in flight from the start: B's latency hides under A's transposes
+    double2 vb[WR];
+    gd2* XA = gptr(W.vec_a);
+    gd2* XB = gptr(W.vec_b);
 #pragma unroll
-      for (int r = 0; r < WR; ++r) v[r] = gld(X, ia[r]);
-      tile_fwd<WL>(S.w, v, G.c, tid);
+    for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
 #pragma unroll
-      for (int r = 0; r < WR; ++r) gst(X, is[r], v[r]);
-    }
+    for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
+    tile_fwd<WL>(S.w, v, G.c, tid);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) gst(XA, is[r], v[r]);
+    tile_fwd<WL>(S.w, vb, G.c, tid);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) gst(XB, is[r], vb[r]);
     return;
   }
 
