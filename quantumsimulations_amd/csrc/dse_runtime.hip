@@ -527,7 +527,7 @@ int ensure_wht(dse_ctx* ctx) {
     const size_t vbytes = (size_t(1) << nl) * sizeof(double2);
     const int nvec = S > 0 ? 4 : 2;
     bool ok = hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) == hipSuccess &&
-              hipMalloc(&p.d_wtab, (size_t)p.n_tiles * 48 * sizeof(double)) == hipSuccess;
+              hipMalloc(&p.d_wtab, ((size_t)p.n_tiles * 48 + 2 * (5 * 512 + 16)) * sizeof(double)) == hipSuccess;
     for (int v = 0; v < nvec && ok; ++v) ok = hipMalloc(&p.wvec[v], vbytes) == hipSuccess;
     if (!ok)
       return fail(ctx, DSE_ERR_OOM, "device allocation of the Walsh-Hadamard vectors failed (" +
@@ -548,6 +548,7 @@ int ensure_wht(dse_ctx* ctx) {
     w.cquad = p.d_cquad;
     w.ztab = p.d_wtab;
     w.xytab = p.d_wtab + (size_t)p.n_tiles * 16;
+    w.qtab = p.d_wtab + (size_t)p.n_tiles * 48;
     w.n = n;
     w.n_local = nl;
     w.wl = p.L;

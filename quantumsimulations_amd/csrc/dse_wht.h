@@ -40,6 +40,10 @@ struct WhtProb {
   // per-tile coefficient tables (launch_wht_tables), one row per outer index o:
   double* ztab;           // [tiles][16] group 0: F_i(o) i < WL, C(o) without beta (D_Z, s = 1/2 - bit)
   double* xytab;          // [tiles][32] MID group: F^X_q(o), C^X(o) at 0..WL, F^Y, C^Y at 16..16+WL
+  // Tile-independent pair forms per thread (launch_wht_tables): form 0 = MID's in-tile pair
+  // couplings in MID's diagonal layout, form 1 = FINAL's in-tile zz / 4 in layout B; each
+  // [5][NT] (qt, qh[0..3] of every thread) then zr[16] (register-register part per r).
+  double* qtab;
   double lin_x[kWhtMaxQubits];  // Re c_1 of the drive of bit b, * 2^-n
   double lin_y[kWhtMaxQubits];  // Im c_1, * 2^-n
   int n;                  // qubits of the whole register

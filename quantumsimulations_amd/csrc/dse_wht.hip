@@ -166,53 +166,35 @@ template <int WL>
 struct WhtShared {
   double2 w[WG<WL>::SLOTS];
   double f[2][WL + 1];  // MID: D_X, D_Y fields per tile bit + constant; FINAL: D_Z (z convention)
-  double cq[WL * WL];   // in-tile couplings (symmetric, z convention): MID pairs / FINAL zz / 4
-  double zr[WR];        // register-register part of the quadratic form in the diagonal's layout
 };
+
+// size of one pair form in WhtProb::qtab
+template <int WL>
+constexpr int kQForm = 5 * WG<WL>::NT + WR;
 
 __device__ __forceinline__ double zsign(uint64_t v, int b) { return ((v >> b) & 1ull) ? -1.0 : 1.0; }
 
-// zr[r] of layout lay (needs S.cq after a barrier)
+// linear part f[WL] + sum_q f[q] z_q of this thread's amplitudes in layout lay:
+// lt + sum_i lh[i] z_i(r)
 template <int WL>
-__device__ __forceinline__ void tile_zr(WhtShared<WL>& S, int lay, int tid) {
-  if (tid < WR) {
-    double v = 0.0;
-    for (int a = 0; a < 4; ++a)
-      for (int b = a + 1; b < 4; ++b)
-        v += S.cq[reg_tbit<WL>(lay, a) * WL + reg_tbit<WL>(lay, b)] * (zsign(tid, a) * zsign(tid, b));
-    S.zr[tid] = v;
-  }
+__device__ __forceinline__ void lin_parts(const double* f, int lay, int tid, double& lt, double* lh) {
+  lt = f[WL];
+#pragma unroll
+  for (int j = 0; j < WG<WL>::LGNT; ++j) lt += f[thr_tbit<WL>(lay, j)] * zsign(tid, j);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) lh[i] = f[reg_tbit<WL>(lay, i)];
+}
+// pair form of this thread from qtab: qt + sum_i qh[i] z_i(r) + zr[r]
+template <int WL>
+__device__ __forceinline__ void pair_parts(const double* form, int tid, double& qt, double* qh) {
+  const gdbl* q = gptr(form);
+  qt = q[tid];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qh[i] = q[(1 + i) * WG<WL>::NT + tid];
 }
 
-// Per-thread pieces of a quadratic form in layout lay (z_q = +-1 of tile bit q):
-//   linear  f[WL] + sum_q f[q] z_q          -> lt + sum_i lh[i] z_i(r)   (f = nullptr: none)
-//   pairs   sum_{q<q'} cq[q][q'] z_q z_q'   -> qt + sum_i qh[i] z_i(r) + zr[r]
-template <int WL>
-__device__ __forceinline__ void quad_parts(const double* f, const double* cq, int lay, int tid, double& lt,
-                                           double* lh, double& qt, double* qh) {
-  constexpr int LG = WG<WL>::LGNT;
-  lt = f[WL];
-  qt = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    lh[i] = f[reg_tbit<WL>(lay, i)];
-    qh[i] = 0.0;
-  }
-#pragma unroll
-  for (int j = 0; j < LG; ++j) {
-    const int qj = thr_tbit<WL>(lay, j);
-    const double zj = zsign(tid, j);
-    lt += f[qj] * zj;
-    double a = 0.0;
-#pragma unroll
-    for (int i = j + 1; i < LG; ++i) a += cq[qj * WL + thr_tbit<WL>(lay, i)] * zsign(tid, i);
-    qt += a * zj;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) qh[i] += cq[qj * WL + reg_tbit<WL>(lay, i)] * zj;
-  }
-}
-__device__ __forceinline__ double quad_at(double zt, const double* hr, const double* zr, double sg, int r) {
-  double d = zt + sg * zr[r];
+__device__ __forceinline__ double quad_at(double zt, const double* hr, double zr_r, double sg, int r) {
+  double d = zt + sg * zr_r;
 #pragma unroll
   for (int i = 0; i < 4; ++i) d += ((r >> i) & 1 ? -1.0 : 1.0) * hr[i];
   return d;
@@ -238,19 +220,20 @@ __device__ __forceinline__ uint64_t outer_bits(const WhtGroup& G, uint64_t o) {
 template <int WL>
 struct LayIdx {
   uint64_t xt;
-  uint64_t xr[WR];
+  uint64_t rb[4];  // global index bit of each register bit (wave-uniform: scalar registers)
   __device__ __forceinline__ LayIdx(const WhtGroup& G, int lay, int tid, uint64_t xo) {
     xt = xo;
     for (int j = 0; j < WG<WL>::LGNT; ++j) xt |= (uint64_t)((tid >> j) & 1) << G.pos[thr_tbit<WL>(lay, j)];
 #pragma unroll
-    for (int r = 0; r < WR; ++r) {
-      uint64_t a = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a |= (uint64_t)((r >> i) & 1) << G.pos[reg_tbit<WL>(lay, i)];
-      xr[r] = a;
-    }
+    for (int i = 0; i < 4; ++i) rb[i] = uint64_t(1) << G.pos[reg_tbit<WL>(lay, i)];
   }
-  __device__ __forceinline__ uint64_t operator[](int r) const { return xt | xr[r]; }
+  __device__ __forceinline__ uint64_t operator[](int r) const {
+    uint64_t x = xt;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((r >> i) & 1) x |= rb[i];
+    return x;
+  }
 };
 
 // group 0 (pos = identity): global index = o << WL | tau, the register part an immediate
@@ -329,56 +312,49 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
 
   if (PASS == WHT_MID) {
     const int last = has_b<WL>(G.c) ? 1 : 0;
-    {
-      const gd2* XA = gptr((const double2*)W.vec_at);  // in flight under the staging
+    // both vectors in flight from the start (the diagonal needs no staged couplings: the pair
+    // form is a per-thread table, the linear parts one 256-B row per tile)
+    double2 vb[WR];
+    gd2* XA = gptr(W.vec_at);
+    gd2* XB = gptr(W.vec_bt);
 #pragma unroll
-      for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+    for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
+    if (tid < 32) {
+      const double c = gptr((const double*)W.xytab)[o * 32 + tid];
+      if (tid <= WL) S.f[0][tid] = c;
+      else if (tid >= 16 && tid <= 16 + WL) S.f[1][tid - 16] = c;
     }
-    {
-      const gdbl* cq = gptr(W.cquad);
-      for (int e = tid; e < WL * WL; e += WG<WL>::NT)
-        S.cq[e] = cq[W.gmap[G.pos[e / WL]] * W.n + W.gmap[G.pos[e % WL]]];
-      if (tid < 32) {
-        const double c = gptr((const double*)W.xytab)[o * 32 + tid];
-        if (tid <= WL) S.f[0][tid] = c;
-        else if (tid >= 16 && tid <= 16 + WL) S.f[1][tid - 16] = c;
+    double qt, qh[4];
+    pair_parts<WL>(W.qtab, tid, qt, qh);
+    const double* zr = W.qtab + 5 * WG<WL>::NT;
+    __syncthreads();  // S.f
+    // D_X = lin_X + Q, D_Y = lin_Y - Q; each branch's pieces formed when it needs them
+    auto diag = [&](double2* x, int vec) {
+      const double sg = vec == 0 ? 1.0 : -1.0;
+      double lt, lh[4];
+      lin_parts<WL>(S.f[vec], last, tid, lt, lh);
+      lt += sg * qt;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lh[i] += sg * qh[i];
+#pragma unroll
+      for (int r = 0; r < WR; ++r) {
+        const double d = quad_at(lt, lh, zr[r], sg, r);
+        x[r].x *= d;
+        x[r].y *= d;
       }
-      __syncthreads();
-      tile_zr<WL>(S, last, tid);
-    }
-    // D_X = lin_X + Q, D_Y = lin_Y - Q (Q: the pair form, shared)
-    double xt, xh[4], yt, yh[4], qt, qh[4];
-    quad_parts<WL>(S.f[0], S.cq, last, tid, xt, xh, qt, qh);
-    {
-      double q2, qh2[4];
-      quad_parts<WL>(S.f[1], S.cq, last, tid, yt, yh, q2, qh2);
-    }
-    __syncthreads();  // S.zr
-#pragma unroll 1
-    for (int vec = 0; vec < 2; ++vec) {
-      gd2* X = gptr(vec == 0 ? W.vec_at : W.vec_bt);
-      if (vec == 1) {
+    };
+    tile_fwd<WL>(S.w, v, G.c, tid);
+    diag(v, 0);
+    tile_back<WL>(S.w, v, G.c, last, tid);
 #pragma unroll
-        for (int r = 0; r < WR; ++r) v[r] = gld(X, ia[r]);
-      }
-      tile_fwd<WL>(S.w, v, G.c, tid);
-      {
-        const double sg = vec == 0 ? 1.0 : -1.0;
-        double h[4];
-        const double t0 = (vec == 0 ? xt : yt) + sg * qt;
+    for (int r = 0; r < WR; ++r) gst(XA, ia[r], v[r]);
+    tile_fwd<WL>(S.w, vb, G.c, tid);
+    diag(vb, 1);
+    tile_back<WL>(S.w, vb, G.c, last, tid);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) h[i] = (vec == 0 ? xh[i] : yh[i]) + sg * qh[i];
-#pragma unroll
-        for (int r = 0; r < WR; ++r) {
-          const double d = quad_at(t0, h, S.zr, sg, r);
-          v[r].x *= d;
-          v[r].y *= d;
-        }
-      }
-      tile_back<WL>(S.w, v, G.c, last, tid);
-#pragma unroll
-      for (int r = 0; r < WR; ++r) gst(X, ia[r], v[r]);
-    }
+    for (int r = 0; r < WR; ++r) gst(XB, ia[r], vb[r]);
     return;
   }
 
@@ -386,19 +362,11 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   if (PASS == WHT_FINAL) {
     constexpr int last = 1;  // group 0 ends every forward transform in layout B
     const LayIdx0<WL> ia0(0, tid, o);
-    // D_Z in the z convention: fields F_i / 2, constant C(h) - beta, in-tile zz / 4
-    {
-      if (tid <= WL) {
-        const double c = gptr((const double*)W.ztab)[o * 16 + tid];
-        S.f[0][tid] = tid == WL ? (MODE == MODE_APPLY ? c : c - P.beta) : 0.5 * c;
-      }
-      const gdbl* zz = gptr(P.zz);
-      for (int e = tid; e < WL * WL; e += WG<WL>::NT) {
-        const int a = e / WL, b = e % WL;
-        S.cq[e] = a == b ? 0.0 : 0.25 * (a < b ? zz[a * P.n + b] : zz[b * P.n + a]);
-      }
-      __syncthreads();
-      tile_zr<WL>(S, last, tid);
+    // D_Z in the z convention: fields F_i / 2 and constant C(h) - beta per tile (ztab), the in-tile
+    // zz / 4 form per thread (qtab form 1)
+    if (tid <= WL) {
+      const double c = gptr((const double*)W.ztab)[o * 16 + tid];
+      S.f[0][tid] = tid == WL ? (MODE == MODE_APPLY ? c : c - P.beta) : 0.5 * c;
     }
     double2 out[WR];
     {
@@ -418,21 +386,17 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
       out[r].x = s.x + v[r].x;
       out[r].y = s.y + v[r].y;
     }
-    // D_Z(x) = zt + sum_i hr[i] z_i(r) + zr[r] (linear and pair parts summed, outer loop rolled)
-    double zt = S.f[0][WL], hr[4];
+    // D_Z(x) = zt + sum_i hr[i] z_i(r) + zr[r]  (S.f visible: the transposes' barriers)
+    double zt, hr[4];
+    {
+      double lt, lh[4], qt, qh[4];
+      lin_parts<WL>(S.f[0], last, tid, lt, lh);
+      pair_parts<WL>(W.qtab + kQForm<WL>, tid, qt, qh);
+      zt = lt + qt;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) hr[i] = S.f[0][reg_tbit<WL>(last, i)];
-#pragma unroll 1
-    for (int j = 0; j < WG<WL>::LGNT; ++j) {
-      const int qj = thr_tbit<WL>(last, j);
-      const double zj = zsign(tid, j);
-      double a = S.f[0][qj];
-#pragma unroll 1
-      for (int i = j + 1; i < WG<WL>::LGNT; ++i) a += S.cq[qj * WL + thr_tbit<WL>(last, i)] * zsign(tid, i);
-      zt += a * zj;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hr[i] += S.cq[qj * WL + reg_tbit<WL>(last, i)] * zj;
+      for (int i = 0; i < 4; ++i) hr[i] = lh[i] + qh[i];
     }
+    const double* zrz = W.qtab + kQForm<WL> + 5 * WG<WL>::NT;
     const gd2* win = gptr((const double2*)P.buf[win_role(MODE, k, q)]);
     gd2* psi_b = gptr(P.buf[q ? 2 : 0]);
     gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
@@ -444,7 +408,7 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
 #pragma unroll
     for (int r = 0; r < WR; ++r) {
       const double2 own = gld(win, is[r]);
-      const double d = quad_at(zt, hr, S.zr, 1.0, r);
+      const double d = quad_at(zt, hr, zrz[r], 1.0, r);
       out[r].x = fma(d, own.x, out[r].x);
       out[r].y = fma(d, own.y, out[r].y);
       step_epilogue<MODE>(is[r], out[r], own, scale, wdst, acc_b, C, 0);
@@ -521,6 +485,38 @@ __global__ void __launch_bounds__(256) k_wht_tables(const WhtProb* __restrict__ 
   for (int i = WL + 1; i < 16; ++i) xy[i] = xy[16 + i] = 0.0;
 }
 
+// Tile-independent pair forms (WhtProb::qtab), one block per form, one thread per tile thread.
+template <int WL>
+__global__ void __launch_bounds__(512) k_wht_qtab(const WhtProb* __restrict__ wp, const DevProb* __restrict__ dp) {
+  const WhtProb& W = *wp;
+  const DevProb& P = *dp;
+  const int form = blockIdx.x, tid = threadIdx.x, n = W.n;
+  if (tid >= WG<WL>::NT) return;
+  const WhtGroup& G = W.grp[form == 0 ? W.n_groups - 1 : 0];
+  const int lay = form == 0 ? (has_b<WL>(G.c) ? 1 : 0) : 1;
+  auto cpl = [&](int qa, int qb) -> double {  // coupling of tile bits qa != qb (z convention)
+    if (form == 0) return W.cquad[W.gmap[G.pos[qa]] * n + W.gmap[G.pos[qb]]];
+    const int a = qa < qb ? qa : qb, b = qa < qb ? qb : qa;
+    return 0.25 * P.zz[a * n + b];
+  };
+  double qt = 0.0, qh[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j = 0; j < WG<WL>::LGNT; ++j) {
+    const double zj = zsign(tid, j);
+    for (int i = j + 1; i < WG<WL>::LGNT; ++i)
+      qt += cpl(thr_tbit<WL>(lay, j), thr_tbit<WL>(lay, i)) * zj * zsign(tid, i);
+    for (int i = 0; i < 4; ++i) qh[i] += cpl(reg_tbit<WL>(lay, i), thr_tbit<WL>(lay, j)) * zj;
+  }
+  double* out = W.qtab + form * kQForm<WL>;
+  out[tid] = qt;
+  for (int i = 0; i < 4; ++i) out[(1 + i) * WG<WL>::NT + tid] = qh[i];
+  if (tid < WR) {
+    double v = 0.0;
+    for (int a = 0; a < 4; ++a)
+      for (int b = a + 1; b < 4; ++b) v += cpl(reg_tbit<WL>(lay, a), reg_tbit<WL>(lay, b)) * zsign(tid, a) * zsign(tid, b);
+    out[5 * WG<WL>::NT + tid] = v;
+  }
+}
+
 template <int WL, int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
                        int g, int k, int q, int set, hipStream_t st) {
@@ -556,12 +552,15 @@ hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const D
 
 hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64_t tiles, hipStream_t st) {
   const dim3 grid((unsigned)((tiles + 255) / 256)), block(256);
-  if (wl == 12)
+  if (wl == 12) {
     hipLaunchKernelGGL(k_wht_tables<12>, grid, block, 0, st, wp, dp, tiles);
-  else if (wl == 13)
+    hipLaunchKernelGGL(k_wht_qtab<12>, dim3(2), dim3(512), 0, st, wp, dp);
+  } else if (wl == 13) {
     hipLaunchKernelGGL(k_wht_tables<13>, grid, block, 0, st, wp, dp, tiles);
-  else
+    hipLaunchKernelGGL(k_wht_qtab<13>, dim3(2), dim3(512), 0, st, wp, dp);
+  } else {
     return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
