@@ -61,7 +61,7 @@ def parse():
     return ap.parse_args()
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "v6_m2_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "v7_pmc_traffic.json")
 
 
 def pmc_traffic(kernel: str):
@@ -135,14 +135,24 @@ def large_register(device: int, n_sea: int = 23):
         wall = time.perf_counter() - t0
     per_term_ms = st["step_kernel_ms"] / max(st["timed_launches"], 1)
     gbs = bpa * (1 << n) / (per_term_ms * 1e-3) / 1e9
+    traffic = None  # HBM-side bytes per H application from the committed counter passes (N = 24)
+    try:
+        with open(PMC_TRAFFIC) as f:
+            k = json.load(f)["kernels"]
+        first, mid, fin = k["k_wht<13, 0, 2>"], k["k_wht<13, 2, 2>"], k["k_wht<13, 4, 2>"]
+        # MID reads 64-byte runs at N = 24, which FETCH_SIZE counts in full (no x2 correction)
+        traffic = (first["traffic_bytes_per_launch"] + mid["fetch_bytes_raw"] + mid["write_bytes"]
+                   + fin["traffic_bytes_per_launch"]) if n == 24 else None
+    except (OSError, KeyError, ValueError):
+        pass
     return {
         "workload": f"config 5 on one GPU: N={n} center_on, 50 kHz, t_final 1e-5 s, 11 outputs",
         "engine_mode": st["mode"], "tile_bits": wl, "passes_per_h": 2 * groups - 1,
         "ms_per_h_application": wall / st["h_applications"] * 1e3,
         "kernel_ms_per_h_application": per_term_ms,
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa,
-                     "traffic_source": "profiles/r01/wht_n24_pmc_traffic.json"},
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa, "traffic": traffic,
+                     "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT)},
     }
 
 
