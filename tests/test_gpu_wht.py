@@ -165,3 +165,36 @@ def test_wht_sharded_evolve_matches_unsharded(engine, n, bits, wl):
     for i in range(1 << bits):
         np.testing.assert_allclose(obs[ps + i], ref[p0], rtol=0, atol=1e-12)
     assert np.max(np.abs(s_sh - s_ref)) < 1e-12
+
+
+def test_wht_term_kinds_separately(engine):
+    """Drives only, pairs only, diagonal only: each branch of D_X / D_Y and D_Z on its own."""
+    n = 16
+    base = _random_problem(n, 2100)
+    v = _rand(n, 21)
+    import dataclasses
+    for kind in ("drives", "pairs", "diagonal"):
+        prob = dataclasses.replace(
+            base, flip=base.flip if kind == "drives" else np.zeros_like(base.flip),
+            pair=base.pair if kind == "pairs" else np.zeros_like(base.pair))
+        out = _apply(engine, prob, v, wht=1)
+        ref = rm.bitwise_apply(_tables(prob), v)
+        assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref)), kind
+
+
+def test_wht_mixed_context_matches_separate_evolves(engine):
+    """One context with a small register (step kernels) and a large one (Walsh-Hadamard engine):
+    each evolves exactly as when alone."""
+    small, large = _random_problem(12, 2200, rare_bit=11), _random_problem(16, 2201, rare_bit=15)
+    t = np.linspace(0.0, 2e-4, 4)
+    engine.clear()
+    engine.add(small)
+    engine.add(large)
+    both, st = engine.evolve(t)
+    assert st["mode"] == 2
+    for i, p in enumerate((small, large)):
+        engine.clear()
+        engine.add(p)
+        alone, _ = engine.evolve(t)
+        np.testing.assert_allclose(both[i], alone[0], rtol=0, atol=1e-13)
+    engine.clear()
