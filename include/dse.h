@@ -114,9 +114,10 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "outputs_per_launch"  persistent mode: up to this many (1..2) consecutive output
  *                         times from one Chebyshev series (default 2; 1 on coarse grids,
  *                         alpha dt >= 400)
- *          "wht"          1 (default): streaming registers of more than one tile (n >= 14,
- *                         not sharded) apply H as D_Z + W D_X W + V D_Y V^+ (Walsh-Hadamard
- *                         passes, two extra state-sized vectors per problem); 0: step kernels
+ *          "wht"          1 (default): streaming registers of more than one tile apply H as
+ *                         D_Z + W D_X W + V D_Y V^+ (Walsh-Hadamard passes, two extra state-sized
+ *                         vectors per problem, four per shard of a partitioned register; a problem
+ *                         whose vectors do not fit in HBM keeps the step kernels); 0: step kernels
  *          "wht_tile_bits"   tile of that engine: 12 (two workgroups per CU), 13, or 0 (default:
  *                         13)
  *          "wht_group_bits"  high qubits transformed per pass of that engine, 2..11, or 0

@@ -150,6 +150,14 @@ int fail(dse_ctx* c, int code, const std::string& msg) {
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+void free_wht(HostProblem& p) {
+  for (auto& b : p.wvec)
+    if (b) (void)hipFree(b), b = nullptr;
+  if (p.d_cquad) (void)hipFree(p.d_cquad), p.d_cquad = nullptr;
+  if (p.d_wtab) (void)hipFree(p.d_wtab), p.d_wtab = nullptr;
+  p.wht_groups = 0;
+}
+
 void free_device(dse_ctx* ctx) {
   for (auto& p : ctx->probs) {
     for (auto& b : p.buf)
@@ -159,11 +167,7 @@ void free_device(dse_ctx* ctx) {
     if (p.d_items) (void)hipFree(p.d_items), p.d_items = nullptr;
     for (auto& b : p.rbuf_own)
       if (b) (void)hipFree(b), b = nullptr;
-    for (auto& b : p.wvec)
-      if (b) (void)hipFree(b), b = nullptr;
-    if (p.d_cquad) (void)hipFree(p.d_cquad), p.d_cquad = nullptr;
-    if (p.d_wtab) (void)hipFree(p.d_wtab), p.d_wtab = nullptr;
-    p.wht_groups = 0;
+    free_wht(p);
     p.coef_bytes = 0;
   }
   if (ctx->d_wht) (void)hipFree(ctx->d_wht), ctx->d_wht = nullptr;
@@ -437,6 +441,7 @@ int prepare(dse_ctx* ctx) {
 }
 
 // ---- Walsh-Hadamard engine ------------------------------------------------------------------
+
 // WhtGroup of the given high bits: completed to wl tile bits by the lowest carried bits; every
 // other local bit is an outer bit.
 WhtGroup make_group(const std::vector<int>& bits, int wl, int n_local) {
@@ -529,10 +534,12 @@ int ensure_wht(dse_ctx* ctx) {
     bool ok = hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) == hipSuccess &&
               hipMalloc(&p.d_wtab, ((size_t)p.n_tiles * 48 + 2 * (5 * 512 + 16)) * sizeof(double)) == hipSuccess;
     for (int v = 0; v < nvec && ok; ++v) ok = hipMalloc(&p.wvec[v], vbytes) == hipSuccess;
-    if (!ok)
-      return fail(ctx, DSE_ERR_OOM, "device allocation of the Walsh-Hadamard vectors failed (" +
-                                        std::to_string(nvec * vbytes) + " bytes per problem; option wht = 0 "
-                                        "uses the step kernels)");
+    if (!ok) {  // HBM too small for the engine's two extra vectors: this problem keeps the step kernels
+      (void)hipGetLastError();
+      free_wht(p);
+      std::memset(&w, 0, sizeof(w));
+      continue;
+    }
     HIPC(hipMemcpy(p.d_cquad, cq.data(), cq.size() * sizeof(double), hipMemcpyHostToDevice));
     w.vec_a = p.wvec[0];
     w.vec_b = p.wvec[1];
@@ -554,6 +561,18 @@ int ensure_wht(dse_ctx* ctx) {
     w.wl = p.L;
     w.n_groups = G;
     p.wht_groups = G;
+  }
+  // the shards of a loopback register run the same launches: all on the engine or none
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    const HostProblem& P = ctx->probs[pi];
+    if (P.shard_bits == 0 || P.dist || P.shard_rank != 0) continue;
+    bool all = true;
+    for (int r = 0; r < (1 << P.shard_bits); ++r) all = all && ctx->probs[pi + r].wht_groups > 0;
+    if (all) continue;
+    for (int r = 0; r < (1 << P.shard_bits); ++r) {
+      free_wht(ctx->probs[pi + r]);
+      std::memset(&hw[pi + r], 0, sizeof(WhtProb));
+    }
   }
   if (!ctx->d_wht && hipMalloc(&ctx->d_wht, hw.size() * sizeof(WhtProb)) != hipSuccess)
     return fail(ctx, DSE_ERR_OOM, "device allocation of descriptors failed");
