@@ -118,6 +118,8 @@ bool interval_supported(int L);
 // imag: every drive coefficient of the launched problems is purely imaginary (HostProblem::imag)
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items, int q,
                            int set, int n_out, int* flags, int* err, hipStream_t st);
+// zeroes the interval kernel's hand-off flags of the given items (before a 2-tile launch)
+hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st);
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
                       double* partial, hipStream_t st);
 

@@ -477,7 +477,20 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   }
 }
 
+// hand-off flags of the launched items only (2 per problem: flags[2 * problem + tile]), so the
+// launches of another stream, whose problems' flags are in use, are not disturbed
+__global__ void k_zero_flags(const int2* __restrict__ items, int n_items, int* __restrict__ flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_items) flags[2 * items[i].x + items[i].y] = 0;
+}
+
 }  // namespace
+
+hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st) {
+  if (n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_flags, dim3((n_items + 255) / 256), dim3(256), 0, st, items, n_items, flags);
+  return hipGetLastError();
+}
 
 bool interval_supported(int L) { return L >= kRegBlockMinTile && L <= kMaxTile; }
 

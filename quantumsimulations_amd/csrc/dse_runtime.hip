@@ -1309,7 +1309,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     const HostProblem& P = ctx->probs[order[i]];
     const std::pair<int, int64_t> key(P.L, P.n_tiles);
     int lane = (int)(i % n_lanes);
-    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1) ? 0 : 1;
+    if (persistent) lane = ((P.n_tiles == 2 && P.L == kMaxTile) || n_lanes == 1) ? 0 : 1;
     // shards of one register read each other's vectors: same lane, hence the same launches
     if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);
@@ -1476,7 +1476,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         const int T = 1 << g.L;
         if (persistent) {
           // all K terms of the interval in one launch; 2-tile groups in co-resident chunks
-          if (g.tiles == 2) HIPC(hipMemsetAsync(ctx->d_flags, 0, 2 * ctx->probs.size() * sizeof(int), ln.stream));
+          if (g.tiles == 2) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
           const int64_t cap = g.tiles == 2 ? std::max<int64_t>(2, (ctx->n_cu / 2) * 2) : g.count;
           for (int64_t off = 0; off < g.count; off += cap) {
             const int cnt = (int)std::min<int64_t>(cap, g.count - off);
