@@ -1309,7 +1309,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     const HostProblem& P = ctx->probs[order[i]];
     const std::pair<int, int64_t> key(P.L, P.n_tiles);
     int lane = (int)(i % n_lanes);
-    if (persistent) lane = ((P.n_tiles == 2 && P.L == kMaxTile) || n_lanes == 1) ? 0 : 1;
+    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1) ? 0 : 1;
     // shards of one register read each other's vectors: same lane, hence the same launches
     if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);
