@@ -162,6 +162,13 @@ int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id);
 /* Local state size (amplitudes) of a problem: 2^n, or 2^(n - shard_bits) for a dist shard. */
 int64_t dse_problem_dim(const dse_ctx* ctx, int problem);
 
+/* Diagnostics (host only, no device): the Walsh-Hadamard engine's pass plan for a register of
+ * n_local local qubits (shard_bits of them global), tile_bits 12 or 13, max_bits high qubits per
+ * pass (0: tile_bits - 2).  Writes groups_out[g][0] = carried low bits c, [g][1 + q] = the local
+ * qubit of tile bit q (q < tile_bits), for g < G; returns G (group 0 = FIRST/FINAL, 1..G-2 =
+ * FWD/INV, G-1 = MID), or 0 when the engine cannot take the register. */
+int dse_wht_plan(int n_local, int shard_bits, int tile_bits, int max_bits, int32_t* groups_out /* [4][14] */);
+
 /* ---- hot path ----------------------------------------------------------------------------- */
 /* psi_out = H psi_in for one problem (interleaved complex, 2^n each).  Test/diagnostic hook:
  * runs the same matrix-free tile kernel as the propagator. */

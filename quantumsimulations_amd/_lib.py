@@ -27,7 +27,7 @@ EXPORTED = (
     "dse_create", "dse_create_error", "dse_destroy", "dse_last_error", "dse_set_option",
     "dse_add_problem", "dse_num_problems", "dse_clear", "dse_apply_h", "dse_observables",
     "dse_evolve", "dse_get_state", "dse_time_step_kernel", "dse_add_problem_sharded",
-    "dse_dist_unique_id", "dse_dist_init", "dse_problem_dim",
+    "dse_dist_unique_id", "dse_dist_init", "dse_problem_dim", "dse_wht_plan",
 )
 DSE_DIST_ID_BYTES = 128
 
@@ -89,6 +89,7 @@ def _declare(lib):
         "dse_dist_unique_id": (C.c_int, [C.c_char_p]),
         "dse_dist_init": (C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
         "dse_problem_dim": (C.c_int64, [_vp, C.c_int]),
+        "dse_wht_plan": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -981,6 +981,21 @@ int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id) {
   return DSE_OK;
 }
 
+int dse_wht_plan(int n_local, int shard_bits, int tile_bits, int max_bits, int32_t* groups_out) {
+  if (!groups_out || (tile_bits != 12 && tile_bits != 13) || n_local < 1 || n_local > kWhtMaxQubits ||
+      shard_bits < 0 || shard_bits > kMaxShardBits)
+    return DSE_ERR_ARG;
+  WhtProb w;
+  std::memset(&w, 0, sizeof(w));
+  const int gb = max_bits ? std::min(max_bits, tile_bits - 2) : tile_bits - 2;
+  const int G = wht_layout(n_local, shard_bits, tile_bits, gb, w);
+  for (int g = 0; g < G; ++g) {
+    groups_out[g * 14] = w.grp[g].c;
+    for (int q = 0; q < tile_bits; ++q) groups_out[g * 14 + 1 + q] = w.grp[g].pos[q];
+  }
+  return G;
+}
+
 int64_t dse_problem_dim(const dse_ctx* ctx, int problem) {
   if (!ctx || problem < 0 || problem >= (int)ctx->probs.size()) return DSE_ERR_ARG;
   const HostProblem& P = ctx->probs[problem];

@@ -255,3 +255,53 @@ def test_chebyshev_algorithm_matches_exact_n7(golden, variant):
     for j, k in enumerate(rm.OBS_ORDER):
         np.testing.assert_allclose(got[:, j], tr[f"{variant}_exact_{k}"], rtol=0, atol=1e-11)
     np.testing.assert_allclose(got[:, 6], 1.0, atol=1e-12)
+
+
+def _wht_plan(n_local, shard_bits, wl, max_bits=0):
+    import ctypes as C
+    lib = _lib_or_skip()
+    buf = (C.c_int32 * 56)()
+    G = lib.dse_wht_plan(n_local, shard_bits, wl, max_bits, buf)
+    return G, [(buf[g * 14], list(buf[g * 14 + 1:g * 14 + 1 + wl])) for g in range(max(G, 0))]
+
+
+@pytest.mark.parametrize("wl", [12, 13])
+@pytest.mark.parametrize("shard_bits", [0, 1, 2, 3])
+def test_wht_pass_plans_transform_every_bit_once(wl, shard_bits):
+    """Walsh-Hadamard pass plans (csrc/dse_runtime.hip wht_layout): group 0 is the low tile; every
+    local bit is transformed once (the MID group's top-S positions carry the arriving shard bits,
+    so the top S local bits must leave through an earlier group); carried bits are the lowest ones
+    and groups respect the size limit."""
+    for n_local in range(wl + 1, 35 - shard_bits):
+        for max_bits in (0, 2, 4, 7, 11):
+            G, groups = _wht_plan(n_local, shard_bits, wl, max_bits)
+            mb = min(max_bits or wl - 2, wl - 2)
+            h = n_local - wl
+            if shard_bits == 0:
+                expect = -(-h // mb) + 1
+            elif h < shard_bits or mb <= shard_bits:
+                expect = 0
+            else:
+                m = min(mb - shard_bits, h - shard_bits)
+                expect = -(-(h - m) // mb) + 2
+            assert G == (expect if expect <= 4 else 0)
+            if G == 0:  # the engine cannot take it (the step kernels do)
+                continue
+            assert 2 <= G <= 4
+            c0, pos0 = groups[0]
+            assert c0 == 0 and pos0 == list(range(wl))
+            seen = list(range(wl))
+            for c, pos in groups[1:]:
+                assert 1 <= wl - c <= mb
+                assert pos[:c] == list(range(c))
+                seen += pos[c:]
+            top = list(range(n_local - shard_bits, n_local))
+            if shard_bits == 0:
+                assert sorted(seen) == list(range(n_local))
+            else:
+                pre = [b for c, pos in groups[1:-1] for b in pos[c:]]
+                mid = groups[-1][1][groups[-1][0]:]
+                assert set(top) <= set(pre) and set(top) <= set(mid)
+                # every local bit once before the swap or in MID (T positions count twice: they
+                # are the leaving local bits before and the arriving shard bits in MID)
+                assert sorted(pre + [b for b in mid if b not in top]) == list(range(wl, n_local))
