@@ -17,7 +17,7 @@ Extra fields: "roofline" (dominant kernel: the Chebyshev step, HIP events around
 each launch inside the timed region) and "cpu_baseline" (rank 0, N = 1 only: the
 QuTiP-5 sesolve equivalent -- scipy ZVODE-Adams + CSR, oracle/propagate.py --
 on a bounded sample, extrapolated linearly in simulated time) and "large_register"
-(rank 0, N = 1 only: config 5 on one GPU, N = 24, the Walsh-Hadamard engine's passes
+(rank 0, N = 1 only: config 5 on one GPU, N = 30, the Walsh-Hadamard engine's passes
 against the HBM roofline; --no-large skips it).
 """
 from __future__ import annotations
@@ -112,15 +112,21 @@ def cpu_baseline(budget_s: float):
     }
 
 
-def large_register(device: int, n_sea: int = 23):
-    """Config 5 on one GPU (N = n_sea + 1, center_on, 50 kHz, t_final 1e-5 s, 11 outputs): the
+WHT_PMC_N30 = os.path.join(ROOT, "profiles", "r01", "wht_n30_pmc_traffic.json")
+
+
+def large_register(device: int, n_sea: int = 29):
+    """Config 5 on one GPU (N = n_sea + 1 = 30, center_on, 50 kHz, t_final 5e-6 s, 6 outputs): the
     Walsh-Hadamard engine's H|psi> passes against the HBM roofline.  Bytes per amplitude and H
     application are the passes' algorithmic traffic (FIRST 48, FWD/MID/INV 64 each, FINAL 80 + acc
-    32 every third term), equal to the rocprofv3 FETCH/WRITE counts (profiles/r01/wht_n24_pmc_traffic.json)."""
+    32 every third term); "traffic" is the rocprofv3 FETCH/WRITE count of the same passes
+    (profiles/r01/wht_n30_pmc_traffic.json).  Kernel time per H application from HIP events
+    (excludes the first call's device allocation of 5 x 16 GiB)."""
     from quantumsimulations_amd import problem as pb
     from quantumsimulations_amd.engine import Engine
     from quantumsimulations_amd.sweep import sweep_point_params
-    p = sweep_point_params(n_sea, 50e3, "center_on", 1e-5, 11)
+    t_final, steps = 5e-6, 6
+    p = sweep_point_params(n_sea, 50e3, "center_on", t_final, steps)
     prob = pb.build_problem(p)
     n = prob.n_qubits
     wl = 13
@@ -128,31 +134,28 @@ def large_register(device: int, n_sea: int = 23):
     bpa = 48.0 + 64.0 * (2 * groups - 3) + 80.0 + 32.0 / 3.0
     with Engine(device) as eng:
         eng.add(prob)
-        t = np.linspace(0.0, 1e-5, 11)
-        eng.evolve(t)                                    # warm-up (tables, code objects)
         t0 = time.perf_counter()
-        _, st = eng.evolve(t)
+        _, st = eng.evolve(np.linspace(0.0, t_final, steps))
         wall = time.perf_counter() - t0
     per_term_ms = st["step_kernel_ms"] / max(st["timed_launches"], 1)
     gbs = bpa * (1 << n) / (per_term_ms * 1e-3) / 1e9
-    traffic = None  # HBM-side bytes per H application from the committed counter passes (N = 24)
+    traffic = None  # HBM-side bytes per H application (MODE_GEN passes) from the counter passes
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(WHT_PMC_N30) as f:
             k = json.load(f)["kernels"]
-        first, mid, fin = k["k_wht<13, 0, 2>"], k["k_wht<13, 2, 2>"], k["k_wht<13, 4, 2>"]
-        # MID reads 64-byte runs at N = 24, which FETCH_SIZE counts in full (no x2 correction)
-        traffic = (first["traffic_bytes_per_launch"] + mid["fetch_bytes_raw"] + mid["write_bytes"]
-                   + fin["traffic_bytes_per_launch"]) if n == 24 else None
+        if n == 30:
+            traffic = sum(k[f"k_wht<13, {ps}, 2>"]["traffic_bytes_per_launch"] for ps in range(5))
     except (OSError, KeyError, ValueError):
         pass
     return {
-        "workload": f"config 5 on one GPU: N={n} center_on, 50 kHz, t_final 1e-5 s, 11 outputs",
+        "workload": f"config 5 on one GPU: N={n} center_on, 50 kHz, t_final {t_final} s, {steps} outputs",
         "engine_mode": st["mode"], "tile_bits": wl, "passes_per_h": 2 * groups - 1,
-        "ms_per_h_application": wall / st["h_applications"] * 1e3,
+        "h_applications": st["h_applications"],
         "kernel_ms_per_h_application": per_term_ms,
+        "wall_ms_per_h_application_incl_setup": wall / st["h_applications"] * 1e3,
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa, "traffic": traffic,
-                     "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT)},
+                     "traffic_source": os.path.relpath(WHT_PMC_N30, ROOT)},
     }
 
 
