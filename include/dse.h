@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 4
+#define DSE_ABI_VERSION 5
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -182,6 +182,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
                dse_stats* stats);
 /* Final state of one problem after dse_evolve (2^n interleaved complex). */
 int dse_get_state(dse_ctx* ctx, int problem, double* psi_out);
+/* Energy of the final state after dse_evolve, on the device: e_out[0] = <psi|H|psi> / <psi|psi>,
+ * e_out[1] = <psi|psi> (a partitioned loopback register: shard 0's id, whole register).  Unitary
+ * evolution conserves both exactly, so they check a run whose state is too large to compare
+ * (the reference has no counterpart; its only diagnostic is state_norm, :669).  Not available
+ * for a dist shard (DSE_ERR_ARG). */
+int dse_energy(dse_ctx* ctx, int problem, double* e_out /* [2] */);
 /* Times the Chebyshev step kernel alone: reps launches over all problems, HIP events around
  * each launch.  Returns the mean launch duration and the algorithmic bytes per launch. */
 int dse_time_step_kernel(dse_ctx* ctx, int reps, double* ms_per_launch, double* bytes_per_launch);

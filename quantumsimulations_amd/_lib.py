@@ -20,14 +20,14 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 4
+DSE_ABI_VERSION = 5
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
     "dse_create", "dse_create_error", "dse_destroy", "dse_last_error", "dse_set_option",
     "dse_add_problem", "dse_num_problems", "dse_clear", "dse_apply_h", "dse_observables",
     "dse_evolve", "dse_get_state", "dse_time_step_kernel", "dse_add_problem_sharded",
-    "dse_dist_unique_id", "dse_dist_init", "dse_problem_dim", "dse_wht_plan",
+    "dse_dist_unique_id", "dse_dist_init", "dse_problem_dim", "dse_wht_plan", "dse_energy",
 )
 DSE_DIST_ID_BYTES = 128
 
@@ -82,6 +82,7 @@ def _declare(lib):
         "dse_observables": (C.c_int, [_vp, C.c_int, _dp, _dp]),
         "dse_evolve": (C.c_int, [_vp, _dp, C.c_int, C.c_double, _dp, C.POINTER(DseStats)]),
         "dse_get_state": (C.c_int, [_vp, C.c_int, _dp]),
+        "dse_energy": (C.c_int, [_vp, C.c_int, _dp]),
         "dse_time_step_kernel": (C.c_int, [_vp, C.c_int, _dp, _dp]),
         "dse_add_problem_sharded": (C.c_int, [_vp, C.c_int, _dp, _dp, _dp, _dp, C.c_double,
                                               C.c_uint64, C.c_uint64, C.c_int, C.c_double,

@@ -11,6 +11,8 @@ import os
 import shutil
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -37,24 +39,35 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None) -> str:
-    """Compiles libdse.so (or, with ``out``, a variant library of the same ABI at that path)."""
+    """Compiles libdse.so (or, with ``out``, a variant library of the same ABI at that path).
+    Sources compile to objects in parallel (one hipcc per file), then link."""
     target = out or LIB
     if not force and out is None and not needs_build():
         return LIB
     hipcc = _hipcc()
     tmp = target + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include"),
-           *[os.path.join(CSRC, s) for s in SOURCES],
-           "-L", "/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
-    if verbose and (res.stdout or res.stderr):
-        print(res.stdout + res.stderr)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             "-Wno-unused-function", "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
+    with tempfile.TemporaryDirectory(prefix="dse_build_") as tdir:
+        objs = [os.path.join(tdir, s + ".o") for s in SOURCES]
+        cmds = [[hipcc, *flags, "-c", os.path.join(CSRC, s), "-o", o] for s, o in zip(SOURCES, objs)]
+        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+        with ThreadPoolExecutor(jobs) as ex:
+            results = list(ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds))
+        for c, res in zip(cmds, results):
+            if verbose:
+                print(" ".join(c), flush=True)
+            if res.returncode != 0:
+                raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
+            if verbose and (res.stdout or res.stderr):
+                print(res.stdout + res.stderr)
+        link = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-L", "/opt/rocm/lib",
+                "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp]
+        res = subprocess.run(link, capture_output=True, text=True)
+        if verbose:
+            print(" ".join(link), flush=True)
+        if res.returncode != 0:
+            raise RuntimeError("hipcc link failed:\n" + res.stdout + res.stderr)
     os.replace(tmp, target)
     return target
 

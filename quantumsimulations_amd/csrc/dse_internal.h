@@ -122,5 +122,8 @@ hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* i
 hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st);
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
                       double* partial, hipStream_t st);
+// partial[2 * block + {0, 1}] = block sums of Re(conj(a) b) and |a|^2 over n amplitudes
+hipError_t launch_dot(const double2* a, const double2* b, size_t n, double* partial, int blocks,
+                      hipStream_t st);
 
 }  // namespace dse

@@ -453,6 +453,35 @@ hipError_t launch_obs_L(const DevProb* probs, const int2* items, int n_items, in
   return hipGetLastError();
 }
 
+// <a|b> pieces for dse_energy: per block sum Re(conj(a) b) and sum |a|^2 over a grid-stride
+// range (fixed grid, fixed order: bitwise deterministic).
+__global__ void __launch_bounds__(256)
+k_dot(const double2* __restrict__ a, const double2* __restrict__ b, size_t n, double* __restrict__ partial) {
+  __shared__ double s_red[4][2];
+  const gd2* ga = gptr(a);
+  const gd2* gb = gptr(b);
+  double e = 0.0, q = 0.0;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const double2 x = gld(ga, i), y = gld(gb, i);
+    e += x.x * y.x + x.y * y.y;
+    q += x.x * x.x + x.y * x.y;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    e += __shfl_xor(e, off, 64);
+    q += __shfl_xor(q, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_red[threadIdx.x >> 6][0] = e;
+    s_red[threadIdx.x >> 6][1] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
+    partial[2 * blockIdx.x + 1] = s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1];
+  }
+}
+
 }  // namespace
 
 #define DSE_TILE_CASES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13)
@@ -479,6 +508,12 @@ hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_item
 #undef X
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_dot(const double2* a, const double2* b, size_t n, double* partial, int blocks,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(k_dot, dim3(blocks), dim3(256), 0, st, a, b, n, partial);
+  return hipGetLastError();
 }
 
 }  // namespace dse

@@ -1031,6 +1031,27 @@ int hook_members(dse_ctx* ctx, int problem, int* first, int* count) {
   return DSE_OK;
 }
 
+// buf[1] = H buf[0] for the members [first, first + count) of one register (the engine that
+// evolves it: Walsh-Hadamard passes or the step kernels; dist shards exchange first).
+int apply_members(dse_ctx* ctx, int first, int count, hipStream_t st) {
+  int rc;
+  if ((rc = ensure_wht(ctx))) return rc;
+  if (ctx->probs[first].wht_groups) {  // all members alike
+    const HostProblem& P0 = ctx->probs[first];
+    std::vector<std::pair<const int2*, int>> segs;
+    for (int i = 0; i < count; ++i) segs.push_back({ctx->probs[first + i].d_items, (int)ctx->probs[first + i].n_tiles});
+    std::vector<int> regs;
+    if (P0.shard_bits > 0) regs.push_back(first);
+    return wht_run(ctx, P0.L, P0.wht_groups, segs, regs, MODE_APPLY, 0, 0, 0, st);
+  }
+  if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
+  for (int i = 0; i < count; ++i) {
+    HostProblem& P = ctx->probs[first + i];
+    HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
+  }
+  return DSE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1051,21 +1072,7 @@ int dse_apply_h(dse_ctx* ctx, int problem, const double* psi_in, double* psi_out
     const size_t amps = size_t(1) << P.n_local;
     HIPC(hipMemcpyAsync(P.buf[0], in + i * amps, amps * sizeof(double2), hipMemcpyHostToDevice, st));
   }
-  if ((rc = ensure_wht(ctx))) return rc;
-  if (ctx->probs[first].wht_groups) {  // all members alike
-    const HostProblem& P0 = ctx->probs[first];
-    std::vector<std::pair<const int2*, int>> segs;
-    for (int i = 0; i < count; ++i) segs.push_back({ctx->probs[first + i].d_items, (int)ctx->probs[first + i].n_tiles});
-    std::vector<int> regs;
-    if (P0.shard_bits > 0) regs.push_back(first);
-    if ((rc = wht_run(ctx, P0.L, P0.wht_groups, segs, regs, MODE_APPLY, 0, 0, 0, st))) return rc;
-  } else {
-    if (ctx->probs[first].dist && (rc = dist_exchange(ctx, 0, 0, st))) return rc;
-    for (int i = 0; i < count; ++i) {
-      HostProblem& P = ctx->probs[first + i];
-      HIPC(launch_step(P.L, MODE_APPLY, ctx->d_probs, P.d_items, (int)P.n_tiles, 0, 0, 0, st));
-    }
-  }
+  if ((rc = apply_members(ctx, first, count, st))) return rc;
   for (int i = 0; i < count; ++i) {
     HostProblem& P = ctx->probs[first + i];
     const size_t amps = size_t(1) << P.n_local;
@@ -1637,6 +1644,47 @@ int dse_get_state(dse_ctx* ctx, int problem, double* psi_out) {
     const size_t amps = size_t(1) << P.n_local;
     HIPC(hipMemcpy(out + i * amps, P.buf[bsel], amps * sizeof(double2), hipMemcpyDeviceToHost));
   }
+  return DSE_OK;
+}
+
+int dse_energy(dse_ctx* ctx, int problem, double* e_out) {
+  if (!ctx) return DSE_ERR_ARG;
+  if (!e_out) return fail(ctx, DSE_ERR_ARG, "null pointer");
+  if (!ctx->evolved) return fail(ctx, DSE_ERR_STATE, "no evolved state (call dse_evolve first)");
+  int first = 0, count = 1;
+  int rc = hook_members(ctx, problem, &first, &count);
+  if (rc) return rc;
+  if (ctx->probs[first].dist) return fail(ctx, DSE_ERR_ARG, "dse_energy: not available for a dist shard");
+  HIPC(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->lanes[0].stream;
+  const int bsel = ctx->last_q ? 2 : 0;
+  for (int i = 0; i < count; ++i) {  // H reads buf[0]: copy the state there (it stays in buf[bsel])
+    HostProblem& P = ctx->probs[first + i];
+    if (bsel != 0)
+      HIPC(hipMemcpyAsync(P.buf[0], P.buf[bsel], (size_t(1) << P.n_local) * sizeof(double2),
+                          hipMemcpyDeviceToDevice, st));
+  }
+  if ((rc = apply_members(ctx, first, count, st))) return rc;
+  constexpr int kBlocks = 1024;
+  double* d = nullptr;
+  HIPC(hipMalloc(&d, (size_t)count * kBlocks * 2 * sizeof(double)));
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < count && e == hipSuccess; ++i) {
+    const HostProblem& P = ctx->probs[first + i];
+    e = launch_dot(P.buf[0], P.buf[1], size_t(1) << P.n_local, d + (size_t)i * kBlocks * 2, kBlocks, st);
+  }
+  std::vector<double> h((size_t)count * kBlocks * 2);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d, h.size() * sizeof(double), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d);
+  HIPC(e);
+  double en = 0.0, n2 = 0.0;
+  for (size_t b = 0; b < h.size(); b += 2) {
+    en += h[b];
+    n2 += h[b + 1];
+  }
+  e_out[0] = n2 > 0.0 ? en / n2 : 0.0;
+  e_out[1] = n2;
   return DSE_OK;
 }
 

@@ -152,6 +152,12 @@ class Engine:
         self._check(self._L.dse_get_state(self._h, pid, _lib.ptr(out)))
         return out
 
+    def energy(self, pid: int) -> Tuple[float, float]:
+        """(<psi|H|psi> / <psi|psi>, <psi|psi>) of the final state after evolve, on the device."""
+        out = np.empty(2)
+        self._check(self._L.dse_energy(self._h, pid, _lib.ptr(out)))
+        return float(out[0]), float(out[1])
+
     def time_step_kernel(self, reps: int = 20) -> Tuple[float, float]:
         ms = C.c_double()
         by = C.c_double()

@@ -1,0 +1,86 @@
+"""BASELINE config 3 (N = 14 sweep points) on the production path, against fixtures generated from
+the reference's own Hamiltonian (tests/golden/make_golden_n14.py, hpsi_traces_n14.npz).
+
+* H|v>: the reference-built CSR product at N = 14 for center_off / center_on / shell_off and
+  delta in {0, 75, 150 kHz} (rel 1e-13 of max|Hv|), and <v|O|v> (abs 1e-13).
+* <O>(t): the engine's DEFAULT configuration for a sweep -- every (variant, delta) in one context,
+  engine bit order, the exact center_off reduction -- runs the persistent interval kernel
+  k_interval<13, IMAG=true> (mode 1): center_off as 1-tile registers (13 qubits), center_on as
+  2-tile registers whose crossing term is only the rare drive (raw w hand-off), shell_off as
+  2-tile registers with 13 crossing pairs (generated hand-off).  Traces over 20 outputs (200 us)
+  are held to the reference-H oracle at 1e-10 (north-star target 1e-8), for one and for two
+  output times per launch.
+"""
+import numpy as np
+import pytest
+
+from quantumsimulations_amd import problem as pb
+from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
+
+pytestmark = pytest.mark.gpu
+OBS = ("Ix_sea", "Iy_sea", "Iz_sea", "Iz_R", "Ix_R", "Iy_R")
+DELTAS = (0, 75000, 150000)
+
+
+def _ref_state(dim, seed):
+    """make_golden.rand_state: the fixture's random vector, regenerated from its seed."""
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal(dim) + 1j * rng.standard_normal(dim)
+    return v / np.linalg.norm(v)
+
+
+def _params(variant, delta, t):
+    return sweep_point_params(13, float(delta), variant, float(t[-1]), len(t))
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("delta", DELTAS)
+def test_apply_h_and_observables_match_reference_n14(engine, golden, variant, delta):
+    g = golden("hpsi_traces_n14.npz")
+    key = f"{variant}_{delta}"
+    prob = pb.build_problem(_params(variant, delta, g["t"]), order="reference", reduce=False)
+    assert prob.n_qubits == 14 and prob.psi0_index == int(g[f"{key}_psi0_index"])
+    v = _ref_state(1 << 14, 1400)
+    engine.clear()
+    pid = engine.add(prob)
+    out = engine.apply_h(pid, v)
+    ref = g[f"{key}_Hv"]
+    assert np.max(np.abs(out - ref)) <= 1e-13 * np.max(np.abs(ref))
+    o = engine.observables(pid, v)
+    for j, k in enumerate(OBS):
+        assert abs(o[j] - float(g[f"{key}_expect_{k}"])) < 1e-13, k
+    engine.clear()
+
+
+@pytest.mark.parametrize("m", [2, 1])
+def test_production_interval_kernel_matches_reference_n14(engine, golden, m):
+    g = golden("hpsi_traces_n14.npz")
+    t = g["t"]
+    keys, probs = [], []
+    for variant in VARIANTS:
+        for delta in DELTAS:
+            keys.append(f"{variant}_{delta}")
+            probs.append(pb.build_problem(_params(variant, delta, t)))   # production defaults
+    # the register shapes this test is meant to cover
+    assert [p.n_qubits for p in probs] == [13] * 3 + [14] * 6
+    assert all(p.rare_bit == 13 for p in probs[3:6]) and all(p.rare_bit == 13 for p in probs[6:])
+    assert all(np.all(p.pair[:13, 13] == 0.0) for p in probs[3:6])     # center_on: only the drive crosses
+    assert all(np.count_nonzero(p.pair[:13, 13]) == 13 for p in probs[6:])  # shell_off: 13 pairs cross
+    engine.clear()
+    engine.set_option("outputs_per_launch", m)
+    try:
+        for p in probs:
+            engine.add(p)
+        obs, st = engine.evolve(t)
+    finally:
+        engine.set_option("outputs_per_launch", 2)
+        engine.clear()
+    assert st["mode"] == 1 and st["tile_bits"] == 13 and st["outputs_per_launch"] == m
+    worst = 0.0
+    for i, key in enumerate(keys):
+        for j, k in enumerate(OBS):
+            err = float(np.max(np.abs(obs[i, j] - g[f"{key}_{k}"])))
+            worst = max(worst, err)
+            assert err < 1e-10, (key, k, err)
+        np.testing.assert_allclose(obs[i, 6], g[f"{key}_state_norm"], rtol=0, atol=1e-12)
+    print(f"N=14 production path (M={m}): max |GPU - reference-H oracle| = {worst:.2e}")
