@@ -6,19 +6,26 @@ One "step" = one full batch of the hot path: the 64-detuning x 3-variant sweep
 head-to-head grid t_final = 1e-3 s, 101 output times, with all seven observable
 traces computed.  Problem tables are uploaded before the timed region (inputs
 resident in HBM); each timed step resets every state to psi0 and runs the whole
-evolution (Chebyshev step kernels + observable reductions) to t_final.
+evolution (Chebyshev interval kernels + observable reductions) to t_final.
 
 value = detuning-points / hour over the whole job (points of all ranks / max rank time).
 Multi-GPU (torchrun, one process per GPU): weak scaling; rank r of N takes the
 detunings j = r (mod N) of linspace(0, 150 kHz, 64 N), i.e. 64 distinct points per
 rank, no data-path collective (evolutions are independent).
 
-Extra fields: "roofline" (dominant kernel: the Chebyshev step, HIP events around
-each launch inside the timed region) and "cpu_baseline" (rank 0, N = 1 only: the
-QuTiP-5 sesolve equivalent -- scipy ZVODE-Adams + CSR, oracle/propagate.py --
-on a bounded sample, extrapolated linearly in simulated time) and "large_register"
-(rank 0, N = 1 only: config 5 on one GPU, N = 30, the Walsh-Hadamard engine's passes
-against the HBM roofline; --no-large skips it).
+Extra fields of the JSON line:
+  roofline       the dominant kernel (k_interval, HIP events around every launch on its own
+                 stream inside the timed region) priced as SURVEY.md §8(d) prices a fused
+                 Chebyshev term: 80 B per amplitude per term against the 8 TB/s HBM peak; FP64
+                 rate alongside; "traffic" = the counter-measured bytes per launch
+                 (profiles/<round>/bench_pmc_traffic.json)
+  full_sweep     the reference's own grid (t_final 30 s, 20000 outputs, sweep_sea_detuning.py:
+                 1223-1224) on the same 64 x 3 evolutions: the first few output intervals timed,
+                 extrapolated to all 19999 -> points/hour and ms per ODE step
+  cpu_baseline   rank 0, N = 1 only: the QuTiP-5 sesolve equivalent (oracle/cpu_bench.py) on
+                 the host cores, 1 core and all cores, run before the GPU is touched
+  large_register rank 0, N = 1 only: config 5 on one GPU (N = 30, Walsh-Hadamard engine) against
+                 the HBM roofline, with exact-invariant checks (norm, energy); --no-large skips it
 """
 from __future__ import annotations
 
@@ -58,21 +65,31 @@ def parse():
     ap.add_argument("--n-sea", type=int, default=N_SEA)
     ap.add_argument("--n-det", type=int, default=N_DET)
     ap.add_argument("--no-large", action="store_true", help="skip the config-5 single-GPU leg")
+    ap.add_argument("--no-full", action="store_true", help="skip the reference-grid (30 s) leg")
+    ap.add_argument("--full-intervals", type=int, default=2,
+                    help="output intervals of the 30 s reference grid timed by the full-sweep leg")
+    ap.add_argument("--cpu-cores", type=int, default=int(os.environ.get("DSE_CPU_CORES", "0")),
+                    help="worker processes of the all-core CPU leg (0: this process's CPU share)")
     return ap.parse_args()
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "v7_pmc_traffic.json")
+# rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command (tools/gpu_profile.sh +
+# tools/pmc_summary.py), newest round first
+PMC_TRAFFIC = [os.path.join(ROOT, "profiles", r, f) for r, f in
+               (("r02", "bench_pmc_traffic.json"), ("r01", "v9_pmc_traffic.json"))]
 
 
 def pmc_traffic(kernel: str):
     """HBM-side bytes per launch of ``kernel`` from the committed rocprofv3 counter passes of this
     bench command (FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE), or None."""
-    try:
-        with open(PMC_TRAFFIC) as f:
-            rec = json.load(f)["kernels"][kernel]
-        return rec["traffic_bytes_per_launch"], os.path.relpath(PMC_TRAFFIC, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+    for path in PMC_TRAFFIC:
+        try:
+            with open(path) as f:
+                rec = json.load(f)["kernels"][kernel]
+            return rec["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def flops_per_amp(prob) -> float:
@@ -83,36 +100,32 @@ def flops_per_amp(prob) -> float:
     return 4.0 + 8.0 * n_flips + 2.0 * n_pairs
 
 
-def cpu_baseline(budget_s: float):
-    """QuTiP-5 sesolve equivalent (oracle) on one detuning point, 3 variants, bounded sample."""
-    from oracle import propagate, reference_model as rm
-    import dataclasses
-    from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
-    delta = 75_000.0
-    per_var = budget_s / 3.0
-    total_wall_full = 0.0
-    reached = []
-    for v in VARIANTS:
-        p = sweep_point_params(N_SEA, delta, v, T_FINAL, STEPS_T)
-        H, obs, psi0, _ = rm.build(dataclasses.asdict(p))
-        t = np.linspace(0.0, T_FINAL, STEPS_T)
-        _, info = propagate.zvode_trace(H, psi0, t, obs, atol=1e-10, rtol=1e-9, nsteps=10_000_000,
-                                        max_step=1e-5, time_budget_s=per_var)
-        frac = info["t_reached"] / T_FINAL
-        total_wall_full += info["wall_s"] / max(frac, 1e-12)
-        reached.append(info["t_reached"])
-    pts_per_hour = 3600.0 / total_wall_full
-    return {
-        "value": pts_per_hour, "unit": "detuning-points/hour", "cores": 1, "kind": "port",
-        "sample": (f"ZVODE-Adams (QuTiP-5 sesolve equivalent, oracle/propagate.py) + scipy CSR, "
-                   f"atol 1e-10 rtol 1e-9, N=14, delta=75 kHz, 3 variants, first "
-                   f"{[round(r * 1e6, 1) for r in reached]} us of the {T_FINAL * 1e6:.0f} us grid, "
-                   f"extrapolated linearly in simulated time; 1 core"),
-        "seconds_per_point_extrapolated": total_wall_full,
-    }
+def cpu_baseline(budget_s: float, cores: int):
+    """QuTiP-5 sesolve equivalent on the host cores (oracle/cpu_bench.py), run as a child process
+    before this process touches the GPU (its worker pool forks a process without a GPU context)."""
+    import subprocess
+    if cores <= 0:  # this process's CPU share: the affinity set, capped by the box's thread budget
+        cores = len(os.sched_getaffinity(0))
+        for key in ("OMP_NUM_THREADS", "MAX_JOBS"):
+            if os.environ.get(key, "").isdigit():
+                cores = min(cores, int(os.environ[key]))
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    res = subprocess.run([sys.executable, "-m", "oracle.cpu_bench", "--budget", str(budget_s),
+                          "--cores", str(cores)], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=max(600.0, 20.0 * budget_s))
+    if res.returncode != 0:
+        raise RuntimeError(f"oracle.cpu_bench failed: {res.stderr[-2000:]}")
+    return json.loads(res.stdout.strip().splitlines()[-1])
 
 
 WHT_PMC_N30 = os.path.join(ROOT, "profiles", "r01", "wht_n30_pmc_traffic.json")
+
+
+def diag_energy(prob) -> float:
+    """<psi0|H|psi0> = D(x0) of the basis state psi0 (include/dse.h conventions)."""
+    x = prob.psi0_index
+    sv = np.array([0.5 - ((x >> b) & 1) for b in range(prob.n_qubits)])
+    return float(prob.shift + prob.field @ sv + np.sum(np.triu(prob.zz, 1) * np.outer(sv, sv)))
 
 
 def large_register(device: int, n_sea: int = 29):
@@ -121,7 +134,9 @@ def large_register(device: int, n_sea: int = 29):
     application are the passes' algorithmic traffic (FIRST 48, FWD/MID/INV 64 each, FINAL 80 + acc
     32 every third term); "traffic" is the rocprofv3 FETCH/WRITE count of the same passes
     (profiles/r01/wht_n30_pmc_traffic.json).  Kernel time per H application from HIP events
-    (excludes the first call's device allocation of 5 x 16 GiB)."""
+    (excludes the first call's device allocation of 5 x 16 GiB).  "check": exact invariants of the
+    unitary evolution on the 2^30 state (no reference state exists at this size): ||psi(t)|| = 1 at
+    every output and <H> of the final state = <psi0|H|psi0> (dse_energy, on the device)."""
     from quantumsimulations_amd import problem as pb
     from quantumsimulations_amd.engine import Engine
     from quantumsimulations_amd.sweep import sweep_point_params
@@ -133,10 +148,12 @@ def large_register(device: int, n_sea: int = 29):
     groups = 1 + -(-(n - wl) // (wl - 2))
     bpa = 48.0 + 64.0 * (2 * groups - 3) + 80.0 + 32.0 / 3.0
     with Engine(device) as eng:
-        eng.add(prob)
+        pid = eng.add(prob)
         t0 = time.perf_counter()
-        _, st = eng.evolve(np.linspace(0.0, t_final, steps))
+        obs, st = eng.evolve(np.linspace(0.0, t_final, steps))
         wall = time.perf_counter() - t0
+        energy, norm2 = eng.energy(pid)
+    e0 = diag_energy(prob)
     per_term_ms = st["step_kernel_ms"] / max(st["timed_launches"], 1)
     gbs = bpa * (1 << n) / (per_term_ms * 1e-3) / 1e9
     traffic = None  # HBM-side bytes per H application (MODE_GEN passes) from the counter passes
@@ -147,6 +164,10 @@ def large_register(device: int, n_sea: int = 29):
             traffic = sum(k[f"k_wht<13, {ps}, 2>"]["traffic_bytes_per_launch"] for ps in range(5))
     except (OSError, KeyError, ValueError):
         pass
+    check = {"max_norm_error": float(np.max(np.abs(obs[0, 6] - 1.0))),
+             "energy_rel_error": abs(energy - e0) / abs(e0), "energy": energy, "energy_t0": e0,
+             "final_norm2": norm2}
+    check["ok"] = bool(check["max_norm_error"] < 1e-12 and check["energy_rel_error"] < 1e-11)
     return {
         "workload": f"config 5 on one GPU: N={n} center_on, 50 kHz, t_final {t_final} s, {steps} outputs",
         "engine_mode": st["mode"], "tile_bits": wl, "passes_per_h": 2 * groups - 1,
@@ -156,6 +177,39 @@ def large_register(device: int, n_sea: int = 29):
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa, "traffic": traffic,
                      "traffic_source": os.path.relpath(WHT_PMC_N30, ROOT)},
+        "check": check,
+    }
+
+
+def full_sweep(eng, probs, n_points: int, intervals: int, sync, dist=None):
+    """The reference's grid (sweep_sea_detuning.py:1223-1224: t_final 30 s, 20000 outputs ->
+    dt = 1.5 ms, alpha dt ~ 3e3..1e4: one output per launch, ~1e4 Chebyshev terms each) on the
+    bench's evolutions: one interval untimed (coefficients, warm-up), then the first `intervals`
+    output intervals timed (barrier + device sync around, max over ranks) and extrapolated
+    linearly to all 19999 intervals (every interval has the same length, so the same work)."""
+    t_ref = np.linspace(0.0, 30.0, 20000)
+    eng.evolve(t_ref[:2])
+    stats = []
+    dt = timed_steps(lambda: stats.append(eng.evolve(t_ref[:intervals + 1])[1]), 1, 0, sync, dist)
+    st = stats[-1]
+    per_interval = dt / intervals
+    full_s = per_interval * (len(t_ref) - 1)
+    h_per_ev = st["h_applications"] / len(probs) / intervals     # H applications per evolution
+    k_ms = st["step_kernel_ms"]
+    gbs = 80.0 * st["timed_amp_terms"] / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+    return {
+        "grid": "t_final 30 s, 20000 outputs (sweep_sea_detuning.py:1223-1224)",
+        "intervals_timed": intervals, "s_per_interval": per_interval,
+        "full_sweep_s_extrapolated": full_s,
+        "value": n_points * 3600.0 / full_s, "unit": "detuning-points/hour (extrapolated)",
+        "ms_per_ode_step": per_interval * 1e3 / h_per_ev,
+        "h_applications_per_evolution_per_interval": h_per_ev,
+        "max_degree": st["max_degree"], "outputs_per_launch": st["outputs_per_launch"],
+        "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(st["mode"], "streaming"),
+        "kernel_gbs_80B_per_amp_term": gbs,
+        "kernel_frac_hbm": gbs / HBM_PEAK_GBS if gbs else None,
+        "note": "extrapolated from the timed intervals; the reference's own ZVODE trace of this grid "
+                "takes ~430-1530 h per N=14 evolution on one core (SURVEY.md §6)",
     }
 
 
@@ -195,6 +249,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:  # before any GPU work: the CPU leg forks worker processes
+            cpu = cpu_baseline(args.cpu_budget, args.cpu_cores)
+        except Exception as exc:  # report, never hide
+            cpu = {"value": None, "error": repr(exc)}
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -243,28 +303,36 @@ def main():
     all_flops = sum(s["h_flops"] for s in stats)
     all_bytes = sum(s["step_bytes"] for s in stats)
     fpa = sum(flops_per_amp(p) * (1 << p.n_qubits) for p in probs) / sum(1 << p.n_qubits for p in probs)
+    amp_terms = sum(s["timed_amp_terms"] for s in stats)       # their amplitudes x terms
+    all_amp_terms = sum(s["amplitude_updates"] for s in stats)
     if mode == 1:
-        # persistent interval kernel: the state stays in LDS/registers for all terms of an output
-        # interval; HBM moves only psi (once per interval) -> bounded by FP64 VALU throughput
-        achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
-        traffic, traffic_src = pmc_traffic("k_interval<13, true>") if args.tile_bits == 13 else (None, None)
+        # persistent interval kernel, priced as SURVEY.md §8(d) prices a fused Chebyshev term:
+        # 80 B per amplitude (read w_{k-1}, w_{k-2}, acc; write w_k, acc) against the HBM peak
+        achieved = 80.0 * amp_terms / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+        name = f"k_interval<{args.tile_bits}, true>"
+        traffic, traffic_src = pmc_traffic(name) if args.tile_bits == 13 else (None, None)
+        fp64 = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
         roof = {
-            "kernel": "k_interval<13> (persistent Chebyshev interval: all K terms on chip)",
-            "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "compute": "FP64 VALU (MI355X: FP64 vector peak = dense FP64 MFMA peak = 78.6 TF/s)",
-            "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+            "kernel": f"{name} (persistent Chebyshev interval: all K terms of M outputs on chip)",
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
             "traffic_source": traffic_src,
-            "traffic_rate_gbs": (traffic / (k_ms / k_launches * 1e-3) / 1e9) if (traffic and k_launches) else None,
-            "algorithmic_flops_per_amp": fpa,
+            "bytes_per_amp_term": 80.0,
             "avg_launch_us": k_ms / k_launches * 1e3 if k_launches else None,
-            "flops_per_launch": k_flops / k_launches if k_launches else None,
-            "aggregate_fp64_tflops": all_flops / dt / 1e12,
-            "note": ("the H terms stay on chip (LDS + registers) for a whole launch, so the bound is FP64 "
-                     "issue (with LDS bandwidth close behind), not HBM; traffic = L2<->fabric bytes per "
-                     "launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes, dominated by the 2-tile "
-                     "problems' per-term hand-off; the streaming formulation would move 58.7 B per "
-                     "amplitude per term, i.e. an HBM-equivalent rate of "
-                     f"{all_flops / fpa * 58.7 / dt / 1e9:.0f} GB/s"),
+            "algorithmic_bytes_per_launch": 80.0 * amp_terms / k_launches if k_launches else None,
+            "amp_terms_per_launch": amp_terms / k_launches if k_launches else None,
+            "chip_level": {"achieved": 80.0 * all_amp_terms / dt / 1e9,
+                           "frac": 80.0 * all_amp_terms / dt / 1e9 / HBM_PEAK_GBS,
+                           "note": "all launches of the step (both streams overlap) / step wall time"},
+            "fp64": {"achieved_tflops": fp64, "peak_tflops": FP64_PEAK_TFLOPS,
+                     "frac": fp64 / FP64_PEAK_TFLOPS if fp64 else None,
+                     "algorithmic_flops_per_amp": fpa,
+                     "chip_level_tflops": all_flops / dt / 1e12},
+            "note": ("achieved = 80 B x (amplitudes x Chebyshev terms) of the HIP-event-timed launches / "
+                     "their summed durations (SURVEY.md §8(d)); the terms stay on chip (LDS + "
+                     "registers), so the kernel is bounded by LDS and FP64 issue, not HBM; traffic = "
+                     "L2<->fabric bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                     "(mostly the 2-tile problems' per-term hand-off)"),
         }
     else:
         achieved = k_bytes / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
@@ -312,11 +380,14 @@ def main():
         },
         "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if not args.no_full:
         try:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+            line["full_sweep"] = full_sweep(eng, probs, len(my_det) * world, args.full_intervals,
+                                            torch.cuda.synchronize, dist)
         except Exception as exc:  # report, never hide
-            line["cpu_baseline"] = {"value": None, "error": repr(exc)}
+            line["full_sweep"] = {"error": repr(exc)}
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     eng.close()
     if rank == 0 and world == 1 and not args.no_large:
         try:

@@ -78,6 +78,8 @@ typedef struct dse_stats {
   double h_flops;             /* algorithmic flops of all H applications (4 + 8/drive + 2/pair  */
                               /* per amplitude)                                                 */
   double timed_flops;         /* algorithmic flops of the timed launches                        */
+  double timed_amp_terms;     /* amplitudes x Chebyshev terms of the timed launches (SURVEY.md  */
+                              /* §8(d) prices a fused Chebyshev term at 80 B per amplitude)     */
   int32_t max_degree;         /* largest Chebyshev degree of any problem / interval             */
   int32_t n_intervals;        /* output intervals propagated                                    */
   int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
@@ -85,11 +87,16 @@ typedef struct dse_stats {
   int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel, 
                                  2: streaming with the Walsh-Hadamard engine                     */
   int32_t outputs_per_launch; /* persistent mode: output times per launch (shared series)   */
+  int32_t handoff_fallbacks;  /* evolves of this context re-run on the streaming kernels after  */
+                              /* a cross-tile hand-off timed out (device shared with other work) */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */
 int dse_abi_version(void);
 int dse_device_count(void);                 /* number of HIP devices, 0 if none              */
+/* free_total[0] = free, free_total[1] = total device memory in bytes (hipMemGetInfo), so a caller
+ * can batch evolutions to fit HBM. */
+int dse_device_memory(int device, double* free_total /* [2] */);
 
 /* ---- host-only helpers (no device needed; also used by the tests) ------------------------- */
 /* Rigorous spectral bounds of the H defined by the tables (Weyl's inequality over the 1- and

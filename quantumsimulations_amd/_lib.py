@@ -28,6 +28,7 @@ EXPORTED = (
     "dse_add_problem", "dse_num_problems", "dse_clear", "dse_apply_h", "dse_observables",
     "dse_evolve", "dse_get_state", "dse_time_step_kernel", "dse_add_problem_sharded",
     "dse_dist_unique_id", "dse_dist_init", "dse_problem_dim", "dse_wht_plan", "dse_energy",
+    "dse_device_memory",
 )
 DSE_DIST_ID_BYTES = 128
 
@@ -44,12 +45,14 @@ class DseStats(C.Structure):
         ("wall_ms", C.c_double),
         ("h_flops", C.c_double),
         ("timed_flops", C.c_double),
+        ("timed_amp_terms", C.c_double),
         ("max_degree", C.c_int32),
         ("n_intervals", C.c_int32),
         ("tile_bits", C.c_int32),
         ("streams", C.c_int32),
         ("mode", C.c_int32),
         ("outputs_per_launch", C.c_int32),
+        ("handoff_fallbacks", C.c_int32),
     ]
 
     def as_dict(self):
@@ -83,6 +86,7 @@ def _declare(lib):
         "dse_evolve": (C.c_int, [_vp, _dp, C.c_int, C.c_double, _dp, C.POINTER(DseStats)]),
         "dse_get_state": (C.c_int, [_vp, C.c_int, _dp]),
         "dse_energy": (C.c_int, [_vp, C.c_int, _dp]),
+        "dse_device_memory": (C.c_int, [C.c_int, _dp]),
         "dse_time_step_kernel": (C.c_int, [_vp, C.c_int, _dp, _dp]),
         "dse_add_problem_sharded": (C.c_int, [_vp, C.c_int, _dp, _dp, _dp, _dp, C.c_double,
                                               C.c_uint64, C.c_uint64, C.c_int, C.c_double,

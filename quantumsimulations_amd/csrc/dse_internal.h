@@ -114,7 +114,10 @@ hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items,
                        int k, int q, int set, hipStream_t st);
 hipError_t set_ablate(int mask);
 hipError_t set_ablate_interval(int mask);
+hipError_t set_spin_limit(int limit);
 bool interval_supported(int L);
+// resident workgroups of k_interval<L> per compute unit (occupancy query)
+hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu);
 // imag: every drive coefficient of the launched problems is purely imaginary (HostProblem::imag)
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items, int q,
                            int set, int n_out, int* flags, int* err, hipStream_t st);

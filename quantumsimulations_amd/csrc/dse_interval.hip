@@ -43,9 +43,17 @@ namespace dse {
 
 // Diagnostic ablation mask of k_interval (0 in production), see set_ablate.
 __device__ int g_dse_ablate_iv = 0;
+// Polls of a partner's flag before a hand-off is declared failed (s_sleep 1 between polls:
+// ~0.3 s at the default).  Diagnostics: a negative value fails every hand-off at its first wait,
+// which exercises the runtime's fallback to the streaming kernels.
+__device__ int g_dse_spin_limit = 1 << 22;
 
 hipError_t set_ablate_interval(int mask) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_ablate_iv), &mask, sizeof(int));
+}
+
+hipError_t set_spin_limit(int limit) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_spin_limit), &limit, sizeof(int));
 }
 
 namespace {
@@ -59,7 +67,6 @@ __device__ __forceinline__ cptr<T> cst(const T* p) {
   return (cptr<T>)p;
 }
 
-constexpr int kSpinLimit = 1 << 22;  // ~0.3 s of polling before the hand-off is declared failed
 
 // out += c * s for a drive coefficient c = cr + i ci; IMAG: cr == 0 (drive phase pi/2)
 template <bool IMAG>
@@ -382,9 +389,10 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       if (need_flag) {
         if (tid == 0 && !(ab & 64)) {
           int spins = 0;
-          while (__hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
+          const int limit = g_dse_spin_limit;
+          while (limit < 0 || __hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > kSpinLimit) {
+            if (limit < 0 || ++spins > limit) {
               s_fail = 1;
               atomicExch(err, 1);
               break;
@@ -493,6 +501,21 @@ hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st
 }
 
 bool interval_supported(int L) { return L >= kRegBlockMinTile && L <= kMaxTile; }
+
+hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu) {
+  switch (L) {
+#define X(l)                                                                                       \
+  case l:                                                                                          \
+    return imag ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_interval<l, true>, \
+                                                               RB<l>::NT, 0)                       \
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_interval<l, false>,\
+                                                               RB<l>::NT, 0);
+    X(10) X(11) X(12) X(13)
+#undef X
+    default:
+      return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items,
                            int q, int set, int n_out, int* flags, int* err, hipStream_t st) {

@@ -116,7 +116,9 @@ struct dse_ctx {
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
-  int n_cu = 256;                   // resident workgroups per launch of the 2-tile kernel
+  int n_cu = 256;                   // compute units of the device
+  int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
+  int handoff_fallbacks = 0;        // evolves re-run on the streaming kernels after a hand-off timeout
   int* d_flags = nullptr;           // hand-off flags (2 per problem) + error word
   size_t flags_cap = 0;
   double2* d_xslots = nullptr;      // hand-off slots of the interval kernel
@@ -731,6 +733,21 @@ int dse_device_count(void) {
 
 const char* dse_create_error(void) { return g_create_err.c_str(); }
 
+int dse_device_memory(int device, double* free_total) {
+  if (!free_total) return DSE_ERR_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return DSE_ERR_NODEVICE;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  size_t fr = 0, tot = 0;
+  const bool ok = hipSetDevice(device) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess;
+  (void)hipSetDevice(prev);
+  if (!ok) return DSE_ERR_HIP;
+  free_total[0] = (double)fr;
+  free_total[1] = (double)tot;
+  return DSE_OK;
+}
+
 dse_ctx* dse_create(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -821,8 +838,11 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
       return fail(ctx, DSE_ERR_ARG, "outputs_per_launch must be in 1.." + std::to_string(kMaxOut));
     ctx->outputs_per_launch = (int)value;
   } else if (k == "coresident") {  // diagnostics: workgroups per chunk of a 2-tile interval launch
-    if (!(value >= 2 && value <= 4096)) return fail(ctx, DSE_ERR_ARG, "coresident must be in 2..4096");
-    ctx->n_cu = (int)value;
+    if (!(value == 0 || (value >= 2 && value <= 4096)))
+      return fail(ctx, DSE_ERR_ARG, "coresident must be 0 or in 2..4096");
+    ctx->coresident = (int)value;
+  } else if (k == "spin_limit") {  // diagnostics: partner-flag polls per hand-off (< 0: always fail)
+    HIPC(set_spin_limit((int)value));
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
   } else if (k == "time_kernels") {
@@ -1395,13 +1415,26 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   HIPC(hipMemcpy(ctx->d_items, items.data(), items.size() * sizeof(int2), hipMemcpyHostToDevice));
   bool imag_all = true;
   for (auto& P : ctx->probs) imag_all = imag_all && P.imag;
+  // 2-tile interval launches go out in chunks whose workgroups can all be resident at once (the
+  // pairs hand off every term): the occupancy query x compute units, even.
+  int64_t pair_cap = 2;
+  if (persistent) {
+    int per_cu = 1;
+    if (ctx->coresident > 0) {
+      pair_cap = ctx->coresident;
+    } else {
+      HIPC(interval_occupancy(13, imag_all, &per_cu));
+      pair_cap = (int64_t)std::max(1, per_cu) * ctx->n_cu;
+    }
+    pair_cap = std::max<int64_t>(2, pair_cap / 2 * 2);
+  }
+  const int64_t cap = pair_cap;
   if (persistent) {
     // Interval-kernel order of 2-tile groups: the two tiles of a problem exchange data every
     // term, so place them 8 blocks apart -- blocks b and b + 8 land on one XCD under the
     // observed round-robin dispatch and then hand off through that XCD's L2 (speed only; the
     // hand-off protocol does not depend on placement).  Chunks of one launch are multiples of 16.
     std::vector<int2> iv = items;
-    const int64_t cap = std::max<int64_t>(2, (ctx->n_cu / 2) * 2);
     for (auto& ln : ctx->lanes)
       for (auto& g : ln.groups) {
         if (g.tiles != 2 || !ctx->xcd_pairs) continue;
@@ -1447,13 +1480,21 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64)));
   if ((rc = ensure_partial(ctx, chunk))) return rc;
   if (ctx->time_every > 0)
-    for (auto& ln : ctx->lanes)
-      if ((rc = ensure_events(ctx, ln, (size_t)ln.groups.size() * (ln.max_deg + 1) + 1))) return rc;
+    for (auto& ln : ctx->lanes) {
+      // timed launches per interval and pool: one per term and group (streaming), one per
+      // co-resident chunk and group (persistent); records beyond the pool are skipped, not timed
+      size_t need = 1;
+      for (const auto& g : ln.groups)
+        need += persistent ? (size_t)((g.count + cap - 1) / cap) : (size_t)(ln.max_deg + 1);
+      if ((rc = ensure_events(ctx, ln, need))) return rc;
+    }
 
-  double step_ms = 0.0, launches_timed = 0.0, bytes_timed = 0.0;
+  double step_ms = 0.0, launches_timed = 0.0, bytes_timed = 0.0, amps_timed = 0.0;
   double launches = 0.0, amp_updates = 0.0, all_bytes = 0.0, all_flops = 0.0, flops_timed = 0.0;
-  // per timed launch: algorithmic flops (pool_bytes) and HBM bytes (pool_bytes2, streaming only)
-  std::vector<std::vector<double>> pool_bytes(ctx->lanes.size() * 2), pool_bytes2(ctx->lanes.size() * 2);
+  // per timed launch: algorithmic flops (pool_bytes), HBM bytes (pool_bytes2, streaming only) and
+  // amplitude-terms (pool_amps: amplitudes x Chebyshev terms the launch computes)
+  std::vector<std::vector<double>> pool_bytes(ctx->lanes.size() * 2), pool_bytes2(ctx->lanes.size() * 2),
+      pool_amps(ctx->lanes.size() * 2);
   auto drain = [&](Lane& ln, size_t li, int pool) -> int {
     if (ln.ev_used[pool] == 0) return DSE_OK;
     HIPC(hipEventSynchronize(ln.ev[pool][2 * ln.ev_used[pool] - 1]));
@@ -1462,12 +1503,14 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       HIPC(hipEventElapsedTime(&ms, ln.ev[pool][2 * i], ln.ev[pool][2 * i + 1]));
       step_ms += ms;
       flops_timed += pool_bytes[li * 2 + pool][i];
+      amps_timed += pool_amps[li * 2 + pool][i];
       if (i < pool_bytes2[li * 2 + pool].size()) bytes_timed += pool_bytes2[li * 2 + pool][i];
     }
     launches_timed += (double)ln.ev_used[pool];
     ln.ev_used[pool] = 0;
     pool_bytes[li * 2 + pool].clear();
     pool_bytes2[li * 2 + pool].clear();
+    pool_amps[li * 2 + pool].clear();
     return DSE_OK;
   };
   auto obs_all = [&](int bsel_q, size_t slot) -> int {
@@ -1499,21 +1542,22 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         if (persistent) {
           // all K terms of the interval in one launch; 2-tile groups in co-resident chunks
           if (g.tiles == 2) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
-          const int64_t cap = g.tiles == 2 ? std::max<int64_t>(2, (ctx->n_cu / 2) * 2) : g.count;
-          for (int64_t off = 0; off < g.count; off += cap) {
-            const int cnt = (int)std::min<int64_t>(cap, g.count - off);
+          const int64_t gcap = g.tiles == 2 ? cap : g.count;
+          for (int64_t off = 0; off < g.count; off += gcap) {
+            const int cnt = (int)std::min<int64_t>(gcap, g.count - off);
             double fl = 0.0, am = 0.0;
             for (int64_t i = off; i < off + cnt; ++i) {
               const HostProblem& P = ctx->probs[items[g.off + i].x];
               am += (double)T * P.degree;
               fl += (double)T * P.degree * P.flops_per_amp;
             }
-            if (timed) {
+            if (timed && 2 * ln.ev_used[pool] + 2 <= ln.ev[pool].size()) {
               const size_t i = ln.ev_used[pool]++;
               HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
               HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out, ctx->d_flags, d_err, ln.stream));
               HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
               pool_bytes[li * 2 + pool].push_back(fl);
+              pool_amps[li * 2 + pool].push_back(am);
             } else {
               HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out, ctx->d_flags, d_err, ln.stream));
             }
@@ -1540,13 +1584,14 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
           if (na <= 0) break;
           if (any_dist_step && (rc = dist_exchange(ctx, ((k - 1) & 1) ? 1 : (q ? 2 : 0), k, ln.stream)))
             return rc;
-          if (timed) {
+          if (timed && 2 * ln.ev_used[pool] + 2 <= ln.ev[pool].size()) {
             const size_t i = ln.ev_used[pool]++;
             HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
             if ((rc = step(MODE_GEN, na, k))) return rc;
             HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
             pool_bytes[li * 2 + pool].push_back(g.flops[k]);
             pool_bytes2[li * 2 + pool].push_back(g.bytes[k]);
+            pool_amps[li * 2 + pool].push_back((double)na * T);
           } else {
             if ((rc = step(MODE_GEN, na, k))) return rc;
           }
@@ -1580,7 +1625,21 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   if (persistent) {
     int herr = 0;
     HIPC(hipMemcpy(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (herr) return fail(ctx, DSE_ERR_HIP, "cross-tile hand-off timed out (workgroup pair not co-resident)");
+    if (herr) {
+      // A workgroup pair of a 2-tile problem was not resident together within the spin limit
+      // (the device shared with long-running work of another stream or process): the results of
+      // this call are incomplete, so it runs again on the per-term streaming kernels, which have
+      // no inter-workgroup dependency.
+      const int zero = 0;
+      HIPC(hipMemcpy(d_err, &zero, sizeof(int), hipMemcpyHostToDevice));
+      const int saved = ctx->persistent;
+      ctx->persistent = 0;
+      ctx->handoff_fallbacks += 1;
+      rc = dse_evolve(ctx, t, n_t, tol, obs_out, stats);
+      ctx->persistent = saved;
+      if (stats) stats->handoff_fallbacks = ctx->handoff_fallbacks;
+      return rc;
+    }
   }
   if (any_dist) {  // sums over all shards of the register, then normalisation (finish_obs)
     double* d_raw = nullptr;
@@ -1613,6 +1672,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->step_bytes = all_bytes;
     stats->h_flops = all_flops;
     stats->timed_flops = flops_timed;
+    stats->timed_amp_terms = amps_timed;
     stats->mode = persistent ? 1 : (used_wht ? 2 : 0);
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
     stats->step_launches = launches;
@@ -1624,6 +1684,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->tile_bits = ctx->probs.empty() ? 0 : ctx->probs.front().L;
     stats->streams = n_lanes;
     stats->outputs_per_launch = M;
+    stats->handoff_fallbacks = ctx->handoff_fallbacks;
   }
   return DSE_OK;
 }

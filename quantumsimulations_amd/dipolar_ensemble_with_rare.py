@@ -82,20 +82,30 @@ def simulate_rare_batch(params_list: Sequence[DipolarRareParams], device: int | 
     by_grid: Dict[Tuple[float, int], List[int]] = {}
     for i, p in enumerate(params_list):
         by_grid.setdefault((float(p.t_final), int(p.steps)), []).append(i)
+    from .engine import batches_for_memory
     for key, idxs in by_grid.items():
-        eng.clear()
-        for i in idxs:
-            eng.add(probs[i])
-        t = grids[idxs[0]]
-        obs, _ = eng.evolve(t, tol=_tol())
-        for slot, i in enumerate(idxs):
-            results[i] = (t.copy(), {name: obs[slot, j].copy() for j, name in enumerate(OBS_NAMES)})
+        for batch in batches_for_memory([probs[i] for i in idxs], device):
+            members = [idxs[b] for b in batch]
+            eng.clear()
+            for i in members:
+                eng.add(probs[i])
+            t = grids[members[0]]
+            obs, _ = eng.evolve(t, tol=_tol())
+            for slot, i in enumerate(members):
+                results[i] = (t.copy(), {name: obs[slot, j].copy() for j, name in enumerate(OBS_NAMES)})
     eng.clear()
     return results
 
 
 def simulate_rare(params: DipolarRareParams) -> Tuple[np.ndarray, Dict[str, np.ndarray]]:
-    """Time grid and the six expectation traces + state norm (reference :611-680)."""
+    """Time grid and the six expectation traces + state norm (reference :611-680).
+
+    ``state_norm`` always has length ``steps`` here (||psi(t)|| of the exactly propagated state).
+    The reference computes it from ``res.states`` (:669); when no ``solver_*`` override is set it
+    passes ``options=None`` and QuTiP 5, by its ``store_states`` default with ``e_ops`` given,
+    likely stores no states, so its ``state_norm`` would be empty.  That default cannot be
+    checked offline (QuTiP is absent: parity unpinned); the sweep always sets the overrides
+    (sweep_sea_detuning.py:1247-1250), where both return one norm per output time."""
     return simulate_rare_batch([params])[0]
 
 

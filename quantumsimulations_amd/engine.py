@@ -23,6 +23,40 @@ def device_count() -> int:
     return int(_lib.lib().dse_device_count())
 
 
+def device_memory(device: int) -> Tuple[float, float]:
+    """(free, total) bytes of a device's memory (hipMemGetInfo)."""
+    out = np.empty(2)
+    rc = _lib.lib().dse_device_memory(int(device), _lib.ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"dse_device_memory({device}) failed ({rc})")
+    return float(out[0]), float(out[1])
+
+
+def problem_bytes(prob: Problem) -> float:
+    """Upper estimate of one problem's device footprint in a context: 3 state buffers, one
+    intermediate output of a two-output launch, the Walsh-Hadamard engine's 2 extra vectors or the
+    2-tile hand-off ring (the larger: 2 vectors), plus tables and coefficients."""
+    return 16.0 * (3 + 1 + 2) * (1 << prob.n_qubits) + (4 << 20)
+
+
+def batches_for_memory(probs, device: int, headroom: float = 0.8):
+    """Index batches of ``probs`` whose summed footprint fits ``headroom`` of the free memory of
+    ``device`` (at least one problem per batch; a problem too large alone still gets its own)."""
+    free, _ = device_memory(device)
+    budget = headroom * free
+    out, cur, used = [], [], 0.0
+    for i, p in enumerate(probs):
+        b = problem_bytes(p)
+        if cur and used + b > budget:
+            out.append(cur)
+            cur, used = [], 0.0
+        cur.append(i)
+        used += b
+    if cur:
+        out.append(cur)
+    return out
+
+
 class Engine:
     def __init__(self, device: int = 0, tile_bits: int | None = None, time_kernels: bool = True):
         self._L = _lib.lib()

@@ -28,7 +28,7 @@ import json
 import os
 import threading
 import time
-from dataclasses import asdict, replace
+from dataclasses import asdict, dataclass, replace
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -67,9 +67,14 @@ def assign_lpt(costs: Sequence[float], n_bins: int) -> List[List[int]]:
 
 
 def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequence[int]] = None,
-                tol: float = 1e-14) -> List[Trace]:
+                tol: Optional[float] = None) -> List[Trace]:
     """``simulate_rare`` for every parameter set, spread over ``devices`` (one host thread and one
-    libdse context per GPU; the ctypes call releases the GIL).  Results in input order."""
+    libdse context per GPU; the ctypes call releases the GIL).  Results in input order.  Each
+    device evolves its share in batches that fit its free memory (the reference runs one
+    evolution at a time, so a sweep of large registers must not allocate all of them at once).
+    ``tol``: Chebyshev truncation, default DSE_TOL as in simulate_rare."""
+    from .dipolar_ensemble_with_rare import _tol
+    tol = _tol() if tol is None else float(tol)
     grids = [time_grid(p) for p in params_list]
     probs = [build_problem(p, order="engine", reduce=True) for p in params_list]
     devices = list(devices) if devices is not None else _visible_devices()
@@ -82,7 +87,7 @@ def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequ
     errors: List[BaseException] = []
 
     def work(dev: int, idxs: List[int]) -> None:
-        from .engine import Engine
+        from .engine import Engine, batches_for_memory
         try:
             with Engine(dev) as eng:
                 by_grid: Dict[Tuple[float, int], List[int]] = {}
@@ -91,13 +96,16 @@ def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequ
                                        []).append(i)
                 for group in by_grid.values():
                     eng.clear()
-                    for i in group:
-                        eng.add(probs[i])
-                    t = grids[group[0]]
-                    obs, _ = eng.evolve(t, tol=tol)
-                    for slot, i in enumerate(group):
-                        results[i] = (t.copy(), {name: obs[slot, j].copy()
-                                                 for j, name in enumerate(OBS_NAMES)})
+                    for batch in batches_for_memory([probs[i] for i in group], dev):
+                        eng.clear()
+                        members = [group[b] for b in batch]
+                        for i in members:
+                            eng.add(probs[i])
+                        t = grids[members[0]]
+                        obs, _ = eng.evolve(t, tol=tol)
+                        for slot, i in enumerate(members):
+                            results[i] = (t.copy(), {name: obs[slot, j].copy()
+                                                     for j, name in enumerate(OBS_NAMES)})
         except BaseException as exc:  # re-raised in the caller's thread
             errors.append(exc)
 
@@ -140,7 +148,26 @@ def _variant(base: DipolarRareParams, tag: str) -> DipolarRareParams:
     return replace(base, drive_rare=False, is_center_rare=False)
 
 
-def run_sweep_sea_detuning(
+@dataclass
+class SweepPlan:
+    """Everything of one sweep that precedes its evolutions (sweep_sea_detuning.py:414-610)."""
+    base_dir: str
+    dets: np.ndarray
+    f_Az: float
+    f1A: float
+    f1R: float
+    coarse_window: int
+    rms_b_AR: float
+    global_params: Dict[str, Any]
+    point_params: List[Dict[str, DipolarRareParams]]
+
+    @property
+    def flat(self) -> List[DipolarRareParams]:
+        """The 3 x n_det evolutions, detuning-major in the reference's variant order (:694-702)."""
+        return [pp[tag] for pp in self.point_params for tag in VARIANTS]
+
+
+def plan_sweep(
     *,
     f_Az: float,
     f1A: float,
@@ -160,17 +187,10 @@ def run_sweep_sea_detuning(
     solver_nsteps: int | None = None,
     solver_max_step: float | None = None,
     coarse_window: int = 50,
-    devices: Optional[Sequence[int]] = None,
-    report: str = "full",
-    timings: Optional[Dict[str, float]] = None,
     verbose: bool = True,
-) -> str:
-    """Same arguments, outputs and return value (the sweep directory) as
-    sweep_sea_detuning.py:356-1165, plus ``devices`` (GPU ids, default all visible),
-    ``report`` ("full" | "png" | "none") and ``timings`` (filled with evolve_s / outputs_s /
-    report_s)."""
-    if report not in ("full", "png", "none"):
-        raise ValueError(f"report must be 'full', 'png' or 'none', not {report!r}")
+) -> SweepPlan:
+    """The sweep directory, its geometry file, global parameters and the parameter records of every
+    evolution (:414-668), before any evolution runs."""
     say = print if verbose else (lambda *a, **k: None)
     f1R = f1R_for_resonance(f1A, target_sea_detuning, 0.0)
     dets = np.asarray(sea_detunings_Hz, dtype=float)
@@ -217,8 +237,6 @@ def run_sweep_sea_detuning(
         "rms_b_AA_Hz": float(cs["sea_sea_rms_Hz"]),
     }
     say(f"Sea detuning sweep: {len(dets)} points x 3 variants -> {base_dir}", flush=True)
-
-    # ---- all evolutions of the sweep at once ----
     point_params: List[Dict[str, DipolarRareParams]] = []
     for delta in dets:
         f_rf_sea = f_Az - delta
@@ -227,29 +245,35 @@ def run_sweep_sea_detuning(
                                   dipolar_scale, shell_scale, t_final, steps, is_spin_three_half,
                                   solver)
         point_params.append({tag: _variant(base, tag) for tag in VARIANTS})
-    flat = [pp[tag] for pp in point_params for tag in VARIANTS]
-    t0 = time.perf_counter()
-    traces = evolve_many(flat, devices)
-    t1 = time.perf_counter()
-    say(f"  evolved {len(flat)} evolutions in {t1 - t0:.2f} s", flush=True)
+    return SweepPlan(base_dir, dets, float(f_Az), float(f1A), float(f1R), int(coarse_window),
+                     float(cs["sea_rare_rms_Hz"]), global_params, point_params)
 
-    # ---- per-point files and metrics, in detuning order ----
-    summary: Dict[str, Any] = {"global_params": global_params, "sweep_results": []}
+
+def write_sweep(plan: SweepPlan, traces: Sequence[Trace], report: str = "full",
+                timings: Optional[Dict[str, float]] = None, verbose: bool = True) -> str:
+    """Per-point files and metrics in detuning order, the report, global_params.json and
+    summary.json (:611-1157) from the evolutions' traces (in ``plan.flat`` order)."""
+    if report not in ("full", "png", "none"):
+        raise ValueError(f"report must be 'full', 'png' or 'none', not {report!r}")
+    say = print if verbose else (lambda *a, **k: None)
+    t1 = time.perf_counter()
+    base_dir = plan.base_dir
+    summary: Dict[str, Any] = {"global_params": plan.global_params, "sweep_results": []}
     details = []
-    for idx, delta in enumerate(dets):
+    for idx, delta in enumerate(plan.dets):
         det_dir = os.path.join(base_dir, detuning_label(delta))
         os.makedirs(det_dir, exist_ok=True)
         per = {}
         for j, tag in enumerate(VARIANTS):
             t_arr, obs = traces[3 * idx + j]
-            p = point_params[idx][tag]
+            p = plan.point_params[idx][tag]
             np.savez(os.path.join(det_dir, f"time_and_obs_{tag}.npz"), t=t_arr, **obs)
             _json_dump(os.path.join(det_dir, f"params_{tag}.json"), asdict(p))
             _json_dump(os.path.join(det_dir, f"freqs_{tag}.json"), get_derived_frequencies(p))
             per[tag] = (t_arr, obs)
-        metrics, det = point_metrics(delta, f_Az - delta, f1A, f1R, cs["sea_rare_rms_Hz"],
+        metrics, det = point_metrics(delta, plan.f_Az - delta, plan.f1A, plan.f1R, plan.rms_b_AR,
                                      {k: (v[0], v[1]["Iz_sea"]) for k, v in per.items()},
-                                     coarse_window)
+                                     plan.coarse_window)
         _json_dump(os.path.join(det_dir, "metrics.json"), metrics)
         summary["sweep_results"].append(metrics)
         details.append((det_dir, per, metrics, det))
@@ -257,14 +281,61 @@ def run_sweep_sea_detuning(
 
     if report != "none":
         from . import report as rep
-        rep.write_sweep_report(base_dir, global_params, summary["sweep_results"], details,
+        rep.write_sweep_report(base_dir, plan.global_params, summary["sweep_results"], details,
                                pdf=(report == "full"))
     t3 = time.perf_counter()
 
     _json_dump(os.path.join(base_dir, "global_params.json"), summary["global_params"])
     _json_dump(os.path.join(base_dir, "summary.json"), summary)
     if timings is not None:
-        timings.update(evolve_s=t1 - t0, outputs_s=t2 - t1, report_s=t3 - t2)
-    say(f"Sweep complete: {base_dir} (evolve {t1 - t0:.2f} s, files {t2 - t1:.2f} s, "
-        f"report {t3 - t2:.2f} s)", flush=True)
+        timings.update(outputs_s=t2 - t1, report_s=t3 - t2)
+    say(f"Sweep written: {base_dir} (files {t2 - t1:.2f} s, report {t3 - t2:.2f} s)", flush=True)
+    return base_dir
+
+
+def run_sweep_sea_detuning(
+    *,
+    f_Az: float,
+    f1A: float,
+    target_sea_detuning: float,
+    gamma_sea: float,
+    gamma_rare: float,
+    sea_detunings_Hz: Sequence[float],
+    n_sea: int = 12,
+    t_final: float = 3.0e-2,
+    steps: int = 2000,
+    phi_sea: float = 0.0,
+    phi_rare: float = 0.0,
+    out_root: str = "results",
+    is_spin_three_half: bool = False,
+    solver_atol: float | None = None,
+    solver_rtol: float | None = None,
+    solver_nsteps: int | None = None,
+    solver_max_step: float | None = None,
+    coarse_window: int = 50,
+    devices: Optional[Sequence[int]] = None,
+    report: str = "full",
+    timings: Optional[Dict[str, float]] = None,
+    verbose: bool = True,
+) -> str:
+    """Same arguments, outputs and return value (the sweep directory) as
+    sweep_sea_detuning.py:356-1165, plus ``devices`` (GPU ids, default all visible),
+    ``report`` ("full" | "png" | "none") and ``timings`` (filled with evolve_s / outputs_s /
+    report_s)."""
+    if report not in ("full", "png", "none"):
+        raise ValueError(f"report must be 'full', 'png' or 'none', not {report!r}")
+    plan = plan_sweep(f_Az=f_Az, f1A=f1A, target_sea_detuning=target_sea_detuning,
+                      gamma_sea=gamma_sea, gamma_rare=gamma_rare, sea_detunings_Hz=sea_detunings_Hz,
+                      n_sea=n_sea, t_final=t_final, steps=steps, phi_sea=phi_sea, phi_rare=phi_rare,
+                      out_root=out_root, is_spin_three_half=is_spin_three_half,
+                      solver_atol=solver_atol, solver_rtol=solver_rtol, solver_nsteps=solver_nsteps,
+                      solver_max_step=solver_max_step, coarse_window=coarse_window, verbose=verbose)
+    t0 = time.perf_counter()
+    traces = evolve_many(plan.flat, devices)
+    t1 = time.perf_counter()
+    if verbose:
+        print(f"  evolved {len(plan.flat)} evolutions in {t1 - t0:.2f} s", flush=True)
+    base_dir = write_sweep(plan, traces, report=report, timings=timings, verbose=verbose)
+    if timings is not None:
+        timings["evolve_s"] = t1 - t0
     return base_dir

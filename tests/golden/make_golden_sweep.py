@@ -16,6 +16,9 @@ Fixtures written:
                        t_final 2e-4 s, 60 outputs, coarse_window 5, the sweep's ZVODE tolerances):
                        every .npz and .json of the tree, plus manifest.json listing every file
                        of the tree (PNG / PDF included) relative to the sweep directory
+  sweep2d_c4/          BASELINE config 4 in miniature: the reference's sweeps at f1A = 5 and 20 kHz
+                       (n_sea = 6, 3 detunings in [0, 3 f1A], 4e-4 s, 80 outputs) and its 2D
+                       aggregation over both trees (config4_fixture)
   sweep2d/             synthetic multi-sweep summary.json files (4 f1A values, NaN / missing
                        entries, a sweep without f1A) and expected.json: the reference's
                        aggregate_points, compute_stable_region for several criteria and the
@@ -180,8 +183,61 @@ def sweep2d_fixture():
                    "graphs_make_plots": files_a, "graphs_stable": files_b}, f, indent=1)
 
 
+CONFIG4 = dict(f1a=(5000.0, 20000.0), n_sea=6, n_det=3, t_final=4e-4, steps=80, coarse_window=5)
+
+
+def config4_fixture():
+    """BASELINE config 4 in miniature: the reference's sweep for two drive strengths (its __main__
+    pattern: target = f1A, detunings linspace(0, 3 f1A, n), sweep_sea_detuning.py:1220-1240), then
+    its 2D aggregation over both sweep trees (2D_sweep_report.py:288-303,
+    2D_sweep_report_stable_region.py:260-364).  Stored: the trees' .npz/.json files under
+    sweep2d_c4/root/f1A_<Hz>/sweep/ and expected.json (points, stable-region results)."""
+    import types
+    tk = types.ModuleType("tkinter")
+    tk.filedialog = types.ModuleType("tkinter.filedialog")
+    sys.modules["tkinter"], sys.modules["tkinter.filedialog"] = tk, tk.filedialog
+    stab = _load("ref_2d_sweep_report_stable_region", "2D_sweep_report_stable_region.py")
+    out = os.path.join(HERE, "sweep2d_c4")
+    shutil.rmtree(out, ignore_errors=True)
+    root = os.path.join(out, "root")
+    f_az = 8.1812e7 * 3.0 / (2 * np.pi)
+    with tempfile.TemporaryDirectory() as tmp:
+        for f1a in CONFIG4["f1a"]:
+            base = sweep.run_sweep_sea_detuning(
+                f_Az=f_az, f1A=f1a, target_sea_detuning=f1a, gamma_sea=8.1812e7,
+                gamma_rare=6.976e7, sea_detunings_Hz=np.linspace(0.0, 3.0 * f1a, CONFIG4["n_det"]),
+                n_sea=CONFIG4["n_sea"], t_final=CONFIG4["t_final"], steps=CONFIG4["steps"],
+                phi_sea=np.pi / 2.0, phi_rare=np.pi / 2.0, out_root=os.path.join(tmp, "x"),
+                is_spin_three_half=False, solver_atol=1e-10, solver_rtol=1e-9,
+                solver_nsteps=10_000_000, solver_max_step=1e-5,
+                coarse_window=CONFIG4["coarse_window"])
+            dst_root = os.path.join(root, f"f1A_{int(f1a)}", "sweep")
+            for rt, _, names in os.walk(base):
+                for nm in names:
+                    if nm.endswith((".npz", ".json")):
+                        rel = os.path.relpath(os.path.join(rt, nm), base)
+                        dst = os.path.join(dst_root, rel)
+                        os.makedirs(os.path.dirname(dst), exist_ok=True)
+                        shutil.copyfile(os.path.join(rt, nm), dst)
+            shutil.rmtree(os.path.join(tmp, "x"))
+    pts = stab.aggregate_points(root)
+    x = np.array([p["delta_Hz"] / p["f1A_Hz"] for p in pts])
+    c = np.array([p["contrast"] for p in pts])
+    regions = []
+    for c_min, p_min, dec, neg in ((0.2, 0.8, 3, True), (0.05, 0.5, 1, True), (0.0, 0.5, 2, False)):
+        stats, best = stab.compute_stable_region(x, c, c_min, p_min, dec, require_negative=neg)
+        regions.append({"args": [c_min, p_min, dec, neg], "stats": stats, "best": best})
+    with open(os.path.join(out, "expected.json"), "w") as f:
+        json.dump({"config": {**CONFIG4, "f1a": list(CONFIG4["f1a"])}, "points": pts,
+                   "regions": regions}, f, indent=1)
+
+
 if __name__ == "__main__":
-    metrics_fixture()
-    sweep_fixture()
-    sweep2d_fixture()
+    if "--config4" in sys.argv:
+        config4_fixture()
+    else:
+        metrics_fixture()
+        sweep_fixture()
+        sweep2d_fixture()
+        config4_fixture()
     print("ok")

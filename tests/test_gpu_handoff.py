@@ -1,0 +1,83 @@
+"""Robustness of the persistent kernel's cross-workgroup hand-off (2-tile registers, N = 14).
+
+The two tiles of a 2-tile problem are two workgroups that exchange an operand every Chebyshev
+term through flags in global memory (dse_interval.hip); that needs both to be resident at once.
+Launch chunks are sized by the occupancy query (dse_runtime.hip), and when a partner still does
+not show up within the spin limit (the GPU shared with long-running work) the evolve is re-run on
+the streaming kernels, which have no inter-workgroup dependency.
+"""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from quantumsimulations_amd import problem as pb
+from quantumsimulations_amd.sweep import sweep_point_params
+
+pytestmark = pytest.mark.gpu
+T = np.linspace(0.0, 2e-5, 5)
+
+
+def _two_tile_problems():
+    return [pb.build_problem(sweep_point_params(13, d, v, float(T[-1]), len(T)))
+            for d in (0.0, 150e3) for v in ("center_on", "shell_off")]
+
+
+def test_handoff_failure_falls_back_to_streaming(engine):
+    probs = _two_tile_problems()
+    engine.clear()
+    for p in probs:
+        engine.add(p)
+    ref, st = engine.evolve(T)
+    assert st["mode"] == 1 and st["handoff_fallbacks"] == 0
+    engine.set_option("spin_limit", -1)       # diagnostics: every hand-off wait fails
+    try:
+        got, st2 = engine.evolve(T)
+    finally:
+        engine.set_option("spin_limit", 1 << 22)
+    assert st2["mode"] in (0, 2) and st2["handoff_fallbacks"] >= 1   # streaming (step or WHT)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12)
+    again, st3 = engine.evolve(T)              # the context keeps its persistent mode
+    assert st3["mode"] == 1 and np.array_equal(again, ref)
+    engine.clear()
+
+
+def test_two_tile_launch_beside_a_busy_device(engine):
+    """A second context on another host thread keeps the device busy with long 1-tile interval
+    launches (as lane 1 of a sweep, or another job, would) while this context evolves 2-tile
+    problems: the results are those of the idle device."""
+    from quantumsimulations_amd.engine import Engine
+    probs = _two_tile_problems()
+    engine.clear()
+    for p in probs:
+        engine.add(p)
+    alone, _ = engine.evolve(T)
+    hog = Engine(0)
+    t_hog = np.linspace(0.0, 3e-4, 3)
+    for d in np.linspace(0.0, 150e3, 96):     # 96 one-tile registers (13 qubits), ~1e3 terms per launch
+        hog.add(pb.build_problem(sweep_point_params(13, float(d), "center_off", float(t_hog[-1]), 3)))
+    stop = threading.Event()
+    errors = []
+
+    def busy():
+        try:
+            while not stop.is_set():
+                hog.evolve(t_hog)
+        except BaseException as exc:  # re-raised below
+            errors.append(exc)
+
+    th = threading.Thread(target=busy)
+    th.start()
+    try:
+        time.sleep(0.5)
+        runs = [engine.evolve(T) for _ in range(4)]
+    finally:
+        stop.set()
+        th.join()
+        hog.close()
+        engine.clear()
+    assert not errors, errors
+    for obs, st in runs:
+        assert st["mode"] in (0, 1)
+        np.testing.assert_allclose(obs, alone, rtol=0, atol=1e-12)

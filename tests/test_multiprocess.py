@@ -88,6 +88,7 @@ def test_evolve_many_multi_device(monkeypatch):
     from quantumsimulations_amd.sweep import sweep_params
     from quantumsimulations_amd.sweep_runner import evolve_many
     monkeypatch.setattr(eng_mod, "Engine", _FakeEngine)
+    monkeypatch.setattr(eng_mod, "device_memory", lambda dev: (64e9, 288e9))
     _FakeEngine.log = []
     params = sweep_params(4, np.linspace(0.0, 150e3, 5), 1e-4, 11)
     res = evolve_many(params, devices=[0, 1, 2])
@@ -99,6 +100,24 @@ def test_evolve_many_multi_device(monkeypatch):
         assert list(obs) == ["Ix_sea", "Iy_sea", "Iz_sea", "Iz_R", "Ix_R", "Iy_R", "state_norm"]
 
 
+def test_evolve_many_batches_by_device_memory(monkeypatch):
+    """A device share larger than the free memory is evolved in batches that fit it."""
+    from quantumsimulations_amd import engine as eng_mod
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.sweep import sweep_params
+    from quantumsimulations_amd.sweep_runner import evolve_many
+    monkeypatch.setattr(eng_mod, "Engine", _FakeEngine)
+    params = sweep_params(4, np.linspace(0.0, 150e3, 4), 1e-4, 11)     # 12 evolutions, n <= 5
+    per = max(eng_mod.problem_bytes(pb.build_problem(p)) for p in params)
+    monkeypatch.setattr(eng_mod, "device_memory", lambda dev: (3.2 * per / 0.8, 288e9))
+    _FakeEngine.log = []
+    res = evolve_many(params, devices=[0])
+    sizes = [n for _, n in _FakeEngine.log]
+    assert sum(sizes) == len(params) and max(sizes) <= 3 and len(sizes) >= 4
+    for p, (t, obs) in zip(params, res):
+        np.testing.assert_array_equal(obs["Ix_sea"], pb.build_problem(p).shift)
+
+
 def test_evolve_many_propagates_errors(monkeypatch):
     from quantumsimulations_amd import engine as eng_mod
     from quantumsimulations_amd.sweep import sweep_params
@@ -108,5 +127,6 @@ def test_evolve_many_propagates_errors(monkeypatch):
         def evolve(self, t, tol=1e-14):
             raise RuntimeError("device failure")
     monkeypatch.setattr(eng_mod, "Engine", Boom)
+    monkeypatch.setattr(eng_mod, "device_memory", lambda dev: (64e9, 288e9))
     with pytest.raises(RuntimeError, match="device failure"):
         evolve_many(sweep_params(4, [0.0, 1e3], 1e-4, 5), devices=[0, 1])
