@@ -130,3 +130,31 @@ def test_evolve_many_propagates_errors(monkeypatch):
     monkeypatch.setattr(eng_mod, "device_memory", lambda dev: (64e9, 288e9))
     with pytest.raises(RuntimeError, match="device failure"):
         evolve_many(sweep_params(4, [0.0, 1e3], 1e-4, 5), devices=[0, 1])
+
+
+def test_config4_driver_pipeline_with_fake_engine(monkeypatch, tmp_path):
+    """sweep2d_run: sweeps planned up front, evolutions grouped over the devices, sweep trees written
+    by a worker process while the next group evolves, then the 2D report over the root."""
+    import json
+    import os
+    from quantumsimulations_amd import engine as eng_mod
+    from quantumsimulations_amd.sweep2d_run import run_2d_sweep
+    class Sloped(_FakeEngine):
+        def evolve(self, t, tol=1e-14):
+            obs, st = super().evolve(t, tol)
+            for i, p in enumerate(self.probs):   # Iz_sea(t): a ramp whose slope differs per problem
+                tt = np.asarray(t) * 1e3
+                obs[i, 2] = -1.0 + (1.0 + 0.37 * p.n_qubits + 1e-6 * p.shift) * tt + 0.01 * np.sin(41.0 * tt)
+            return obs, st
+    monkeypatch.setattr(eng_mod, "Engine", Sloped)
+    monkeypatch.setattr(eng_mod, "device_memory", lambda dev: (64e9, 288e9))
+    _FakeEngine.log = []
+    out = run_2d_sweep(str(tmp_path), [5e3, 20e3, 35e3], n_det=4, n_sea=5, t_final=1e-4, steps=11,
+                       coarse_window=2, devices=[0, 1], report="none", group=2, verbose=False)
+    assert out["evolutions"] == 3 * 3 * 4 and out["group"] == 2
+    assert sum(n for _, n in _FakeEngine.log) == 36
+    for d, f1a in zip(out["sweep_dirs"], (5000, 20000, 35000)):
+        assert os.path.basename(os.path.dirname(d)) == f"f1A_{f1a}"
+        s = json.load(open(os.path.join(d, "summary.json")))
+        assert s["global_params"]["f1A_Hz"] == f1a and len(s["sweep_results"]) == 4
+    assert os.path.exists(os.path.join(str(tmp_path), "contrast_vs_coupling_summary.pdf"))

@@ -174,3 +174,24 @@ def test_sweep2d_cli_outputs(tmp_path):
     assert sorted(os.listdir(out_b / "graphs")) == exp["graphs_stable"]
     assert json.load(open(out_b / "stable.json")) == exp["stable_json"]
     assert sweep2d.main([str(tmp_path / "missing")]) == 2
+
+
+# ------------------------------------------------------------------------------------------
+# BASELINE config 4 in miniature (tests/golden/sweep2d_c4): the reference's own sweeps at two
+# f1A values and its 2D aggregation over them
+# ------------------------------------------------------------------------------------------
+def test_sweep2d_config4_reference_trees():
+    """The headless 2D port reproduces the reference's aggregation of the reference's sweep trees."""
+    from quantumsimulations_amd import sweep2d
+    exp = json.load(open(os.path.join(GOLDEN, "sweep2d_c4", "expected.json")))
+    root = os.path.join(GOLDEN, "sweep2d_c4", "root")
+    pts = sweep2d.aggregate_points(root)
+    key = lambda p: (p["f1A_Hz"], p["delta_Hz"])  # noqa: E731  (walk order is the filesystem's)
+    assert json.dumps(sorted(pts, key=key)) == json.dumps(sorted(exp["points"], key=key))
+    x = np.array([p["delta_Hz"] / p["f1A_Hz"] for p in exp["points"]])
+    c = np.array([p["contrast"] for p in exp["points"]])
+    for case in exp["regions"]:
+        c_min, p_min, dec, neg = case["args"]
+        stats, best = sweep2d.compute_stable_region(x, c, c_min, p_min, dec, require_negative=neg)
+        assert json.loads(json.dumps(stats)) == case["stats"]
+        assert json.loads(json.dumps(best)) == case["best"]
