@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 5
+#define DSE_ABI_VERSION 6
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -80,6 +80,8 @@ typedef struct dse_stats {
   double timed_flops;         /* algorithmic flops of the timed launches                        */
   double timed_amp_terms;     /* amplitudes x Chebyshev terms of the timed launches (SURVEY.md  */
                               /* §8(d) prices a fused Chebyshev term at 80 B per amplitude)     */
+  double exchange_bytes;      /* partitioned registers over processes: bytes this rank sent to  */
+                              /* other ranks (index swaps / shard exchanges)                     */
   int32_t max_degree;         /* largest Chebyshev degree of any problem / interval             */
   int32_t n_intervals;        /* output intervals propagated                                    */
   int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
@@ -166,6 +168,16 @@ int dse_add_problem_sharded(dse_ctx* ctx, int n_qubits, const double* field, con
 #define DSE_DIST_ID_BYTES 128
 int dse_dist_unique_id(unsigned char* id_out);
 int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id);
+/* The same with a host transport instead of RCCL (tests, or a deployment without RCCL between
+ * the devices): every exchange is handed to fn on the calling host thread with HOST buffers (the
+ * library stages device data through them; fn must not call back into libdse):
+ *   DSE_XCHG_ALLTOALL      send/recv hold world chunks of `bytes` each, chunk p goes to rank p
+ *   DSE_XCHG_SENDRECV      send `bytes` to rank `peer` and receive `bytes` from it into recv
+ *   DSE_XCHG_ALLREDUCE_F64 sum bytes / 8 doubles in place over all ranks (send == recv)
+ * Every rank issues the same sequence of calls.  fn returns 0 on success. */
+enum dse_exchange_op { DSE_XCHG_ALLTOALL = 1, DSE_XCHG_SENDRECV = 2, DSE_XCHG_ALLREDUCE_F64 = 3 };
+typedef int (*dse_exchange_fn)(void* user, int op, void* send, void* recv, uint64_t bytes, int peer);
+int dse_dist_init_exchange(dse_ctx* ctx, int rank, int world, dse_exchange_fn fn, void* user);
 /* Local state size (amplitudes) of a problem: 2^n, or 2^(n - shard_bits) for a dist shard. */
 int64_t dse_problem_dim(const dse_ctx* ctx, int problem);
 

@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 5
+DSE_ABI_VERSION = 6
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -28,9 +28,12 @@ EXPORTED = (
     "dse_add_problem", "dse_num_problems", "dse_clear", "dse_apply_h", "dse_observables",
     "dse_evolve", "dse_get_state", "dse_time_step_kernel", "dse_add_problem_sharded",
     "dse_dist_unique_id", "dse_dist_init", "dse_problem_dim", "dse_wht_plan", "dse_energy",
-    "dse_device_memory",
+    "dse_device_memory", "dse_dist_init_exchange",
 )
 DSE_DIST_ID_BYTES = 128
+DSE_XCHG_ALLTOALL, DSE_XCHG_SENDRECV, DSE_XCHG_ALLREDUCE_F64 = 1, 2, 3
+# int fn(void* user, int op, void* send, void* recv, uint64_t bytes, int peer)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int)
 
 
 class DseStats(C.Structure):
@@ -46,6 +49,7 @@ class DseStats(C.Structure):
         ("h_flops", C.c_double),
         ("timed_flops", C.c_double),
         ("timed_amp_terms", C.c_double),
+        ("exchange_bytes", C.c_double),
         ("max_degree", C.c_int32),
         ("n_intervals", C.c_int32),
         ("tile_bits", C.c_int32),
@@ -87,6 +91,7 @@ def _declare(lib):
         "dse_get_state": (C.c_int, [_vp, C.c_int, _dp]),
         "dse_energy": (C.c_int, [_vp, C.c_int, _dp]),
         "dse_device_memory": (C.c_int, [C.c_int, _dp]),
+        "dse_dist_init_exchange": (C.c_int, [_vp, C.c_int, C.c_int, EXCHANGE_FN, C.c_void_p]),
         "dse_time_step_kernel": (C.c_int, [_vp, C.c_int, _dp, _dp]),
         "dse_add_problem_sharded": (C.c_int, [_vp, C.c_int, _dp, _dp, _dp, _dp, C.c_double,
                                               C.c_uint64, C.c_uint64, C.c_int, C.c_double,

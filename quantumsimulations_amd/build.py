@@ -18,8 +18,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdse.so")
-SOURCES = ["dse_kernels.hip", "dse_interval.hip", "dse_wht.hip", "dse_runtime.hip", "dse_host.cpp"]
-HEADERS = ["dse_internal.h", "dse_device.h", "dse_wht.h"]
+SOURCES = ["dse_kernels.hip", "dse_interval.hip", "dse_wht.hip", "dse_small.hip", "dse_runtime.hip",
+           "dse_host.cpp"]
+HEADERS = ["dse_internal.h", "dse_device.h", "dse_wht.h", "dse_small.h"]
 ARCH = os.environ.get("DSE_OFFLOAD_ARCH", "gfx950")
 
 

@@ -25,6 +25,14 @@ __device__ __forceinline__ double2 cmad(double2 acc, double cr, double ci, doubl
 
 __device__ __forceinline__ int par32(uint32_t v) { return __popc(v) & 1; }
 
+// constant address space: uniform loads become scalar loads (SGPRs, scalar cache)
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ cptr<T> cst(const T* p) {
+  return (cptr<T>)p;
+}
+
 // Global address-space views: loads through them are global_load (vmcnt only) instead of
 // flat_load (which also counts against lgkmcnt and serialises LDS work).
 typedef double __attribute__((ext_vector_type(2))) dv2;

@@ -58,14 +58,15 @@ hipError_t set_spin_limit(int limit) {
 
 namespace {
 
+#ifndef DSE_PUBLISH_AFTER
+#define DSE_PUBLISH_AFTER 2
+#endif
+// Hand-off flag of term k published after phase 1 or after phase 2 (the sweeps): later gives the
+// write-through stores more time to drain before the per-wave vmcnt(0) wait, earlier gives the
+// partner more slack before it needs the flag (its phase 4).
+constexpr int kPublishAfter = DSE_PUBLISH_AFTER;
+
 typedef __attribute__((address_space(1))) int gint;
-// constant address space: uniform loads become scalar loads (SGPRs, scalar cache)
-template <typename T>
-using cptr = const __attribute__((address_space(4))) T*;
-template <typename T>
-__device__ __forceinline__ cptr<T> cst(const T* p) {
-  return (cptr<T>)p;
-}
 
 
 // out += c * s for a drive coefficient c = cr + i ci; IMAG: cr == 0 (drive phase pi/2)
@@ -308,14 +309,16 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       }
     }
 
-    // ---- publish: the hand-off stores of this term have drained under phase 1 ----
-    if (pair && !(ab & 64) && (xgen || k > 1)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- publish: every wave's hand-off stores of this term have drained (s_waitcnt vmcnt(0)
+    // per wave, then the barrier), then one lane stores the term index as the flag (sc1) ----
+    auto publish = [&]() {
+      if (pair && !(ab & 64) && (xgen || k > 1)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
+    };
+    if (kPublishAfter == 1) publish();
 
     if (!(ab & 512)) {
       // ---- phase 2: thread-bit sweeps ----
@@ -362,6 +365,8 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         }
       }
 
+      if (kPublishAfter == 2) publish();  // the stores drained under phases 1 and 2
+
       // ---- phase 3: pairs between two thread bits ----
 #pragma unroll 1
       for (int p = 0; p < ((ab & 2) ? 0 : n_tt); ++p) {
@@ -379,6 +384,8 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         }
       }
     }
+
+    if (kPublishAfter == 2 && (ab & 512)) publish();
 
     // ---- phase 4: the partner tile's contribution ----
     if (pair && !(ab & 128)) {

@@ -29,6 +29,7 @@
 
 #include "../../include/dse.h"
 #include "dse_internal.h"
+#include "dse_small.h"
 #include "dse_wht.h"
 
 using namespace dse;
@@ -66,6 +67,12 @@ struct HostProblem {
   double* d_cquad = nullptr;
   double* d_wtab = nullptr;  // ztab | xytab
   int wht_groups = 0;        // passes' tile-bit groups; 0: this problem uses the step kernels
+  // small-register engine (dse_small.hip): n <= 9 qubits, whole evolution one wave per problem
+  bool sm = false;           // this evolve runs the problem on that engine
+  double2* sm_coef = nullptr;
+  int* sm_deg = nullptr;
+  size_t sm_coef_bytes = 0, sm_deg_bytes = 0;
+  int final_bsel = 0;        // buffer holding the final state after dse_evolve
 };
 
 // One stream's share of the problems, grouped by tile size.
@@ -132,6 +139,21 @@ struct dse_ctx {
   // partitioned registers over processes: one RCCL communicator, one rank per GPU
   ncclComm_t comm = nullptr;
   int dist_rank = 0, dist_world = 1;
+  // or a host transport (dse_dist_init_exchange): device data staged through host buffers
+  dse_exchange_fn xfn = nullptr;
+  void* xuser = nullptr;
+  std::vector<unsigned char> xsend, xrecv;
+  double xbytes = 0.0;              // bytes this rank sent to other ranks (current evolve)
+  // small-register engine
+  int small = 1;                    // registers of <= 9 qubits run on dse_small.hip
+  int small_chunk = 64;             // output intervals per launch of that engine
+  hipStream_t small_stream = nullptr;
+  SmallProb* d_small = nullptr;
+  size_t small_cap = 0;             // descriptors allocated
+  double* d_small_out = nullptr;    // [problem][n_t][8] raw observable sums
+  size_t small_out_cap = 0;
+  int* d_small_aux = nullptr;       // problem selections per register size, interval -> set map
+  size_t small_aux_cap = 0;
 };
 
 namespace {
@@ -169,6 +191,9 @@ void free_device(dse_ctx* ctx) {
     if (p.d_items) (void)hipFree(p.d_items), p.d_items = nullptr;
     for (auto& b : p.rbuf_own)
       if (b) (void)hipFree(b), b = nullptr;
+    if (p.sm_coef) (void)hipFree(p.sm_coef), p.sm_coef = nullptr;
+    if (p.sm_deg) (void)hipFree(p.sm_deg), p.sm_deg = nullptr;
+    p.sm_coef_bytes = p.sm_deg_bytes = 0;
     free_wht(p);
     p.coef_bytes = 0;
   }
@@ -185,6 +210,10 @@ void free_device(dse_ctx* ctx) {
   ctx->xslot_cap = 0;
   if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
   ctx->xacc_cap = 0;
+  if (ctx->d_small) (void)hipFree(ctx->d_small), ctx->d_small = nullptr;
+  if (ctx->d_small_out) (void)hipFree(ctx->d_small_out), ctx->d_small_out = nullptr;
+  if (ctx->d_small_aux) (void)hipFree(ctx->d_small_aux), ctx->d_small_aux = nullptr;
+  ctx->small_cap = ctx->small_out_cap = ctx->small_aux_cap = 0;
   ctx->zzlo_tables.clear();
   ctx->partial_slots = 0;
   ctx->total_items = 0;
@@ -193,6 +222,11 @@ void free_device(dse_ctx* ctx) {
 }
 
 void destroy_lanes(dse_ctx* ctx) {
+  if (ctx->small_stream) {
+    (void)hipStreamSynchronize(ctx->small_stream);
+    (void)hipStreamDestroy(ctx->small_stream);
+    ctx->small_stream = nullptr;
+  }
   for (auto& ln : ctx->lanes) {
     if (ln.stream) (void)hipStreamSynchronize(ln.stream);
     for (auto& pool : ln.ev)
@@ -212,6 +246,7 @@ int ensure_lanes(dse_ctx* ctx) {
 
 int sync_all(dse_ctx* ctx) {
   for (auto& ln : ctx->lanes) HIPC(hipStreamSynchronize(ln.stream));
+  if (ctx->small_stream) HIPC(hipStreamSynchronize(ctx->small_stream));
   return DSE_OK;
 }
 
@@ -587,6 +622,46 @@ int ensure_wht(dse_ctx* ctx) {
   return DSE_OK;
 }
 
+// ---- exchanges of a register partitioned over processes: RCCL, or the host transport ----
+// all-to-all of equal chunks (chunk p -> rank p), device buffers
+int xchg_alltoall(dse_ctx* ctx, const void* src, void* dst, size_t cbytes, hipStream_t st) {
+  ctx->xbytes += (double)cbytes * (ctx->dist_world - 1);
+  if (!ctx->xfn) {
+    const ncclResult_t r = ncclAllToAll(src, dst, cbytes, ncclUint8, ctx->comm, st);
+    if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+    return DSE_OK;
+  }
+  const size_t total = cbytes * ctx->dist_world;
+  ctx->xsend.resize(total);
+  ctx->xrecv.resize(total);
+  HIPC(hipMemcpyAsync(ctx->xsend.data(), src, total, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  if (ctx->xfn(ctx->xuser, DSE_XCHG_ALLTOALL, ctx->xsend.data(), ctx->xrecv.data(), cbytes, -1) != 0)
+    return fail(ctx, DSE_ERR_HIP, "exchange callback (all-to-all) failed");
+  HIPC(hipMemcpyAsync(dst, ctx->xrecv.data(), total, hipMemcpyHostToDevice, st));
+  HIPC(hipStreamSynchronize(st));
+  return DSE_OK;
+}
+
+// in-place sum over ranks of host doubles
+int xchg_allreduce_host(dse_ctx* ctx, double* v, size_t count, hipStream_t st) {
+  if (ctx->xfn) {
+    if (ctx->xfn(ctx->xuser, DSE_XCHG_ALLREDUCE_F64, v, v, count * sizeof(double), -1) != 0)
+      return fail(ctx, DSE_ERR_HIP, "exchange callback (all-reduce) failed");
+    return DSE_OK;
+  }
+  double* d = nullptr;
+  HIPC(hipMalloc(&d, count * sizeof(double)));
+  hipError_t e = hipMemcpyAsync(d, v, count * sizeof(double), hipMemcpyHostToDevice, st);
+  const ncclResult_t r = ncclAllReduce(d, d, count, ncclFloat64, ncclSum, ctx->comm, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(v, d, count * sizeof(double), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d);
+  if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  HIPC(e);
+  return DSE_OK;
+}
+
 // Index swap of the X/Y vectors of partitioned registers (local top S bits <-> shard bits):
 // chunk p of shard r -> chunk r of shard p; an involution, so back = the same exchange from the
 // swapped copies.  Loopback registers: device copies; one shard per process: RCCL all-to-all.
@@ -600,8 +675,8 @@ int wht_swap(dse_ctx* ctx, const std::vector<int>& regs, bool back, hipStream_t 
       if (P0.dist) {
         const double2* src = P0.wvec[back ? 2 + v : v];
         double2* dst = P0.wvec[back ? v : 2 + v];
-        const ncclResult_t r = ncclAllToAll(src, dst, cbytes, ncclUint8, ctx->comm, st);
-        if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+        const int rc = xchg_alltoall(ctx, src, dst, cbytes, st);
+        if (rc) return rc;
         continue;
       }
       for (int r = 0; r < (1 << S); ++r)
@@ -663,6 +738,7 @@ int flush_partials(dse_ctx* ctx, size_t nslots, size_t t0, int n_t, double* obs_
   HIPC(hipMemcpy(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost));
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     const HostProblem& P = ctx->probs[pi];
+    if (P.sm) continue;  // the small-register engine writes its own sums
     const bool grouped = P.shard_bits > 0 && !P.dist;
     const size_t first_member = grouped ? (size_t)P.group_first : pi;
     const size_t n_members = grouped ? (size_t(1) << P.shard_bits) : 1;
@@ -691,10 +767,27 @@ int dist_exchange(dse_ctx* ctx, int role, int min_degree, hipStream_t st) {
   for (auto& P : ctx->probs) {
     if (!P.dist || P.degree < min_degree || !P.xmasks) continue;
     const size_t bytes = (size_t(1) << P.n_local) * sizeof(double2);
+    if (ctx->xfn) {  // host transport: one blocking send/recv per partner, masks in ascending order
+      ctx->xsend.resize(bytes);
+      ctx->xrecv.resize(bytes);
+      HIPC(hipMemcpyAsync(ctx->xsend.data(), P.buf[role], bytes, hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+      for (int m = 1; m < (1 << P.shard_bits); ++m) {
+        if (!((P.xmasks >> m) & 1u)) continue;
+        ctx->xbytes += (double)bytes;
+        if (ctx->xfn(ctx->xuser, DSE_XCHG_SENDRECV, ctx->xsend.data(), ctx->xrecv.data(), bytes,
+                     ctx->dist_rank ^ m) != 0)
+          return fail(ctx, DSE_ERR_HIP, "exchange callback (send/recv) failed");
+        HIPC(hipMemcpyAsync(P.rbuf_own[m], ctx->xrecv.data(), bytes, hipMemcpyHostToDevice, st));
+        HIPC(hipStreamSynchronize(st));
+      }
+      continue;
+    }
     if (ncclGroupStart() != ncclSuccess) return fail(ctx, DSE_ERR_HIP, "ncclGroupStart failed");
     for (int m = 1; m < (1 << P.shard_bits); ++m) {
       if (!((P.xmasks >> m) & 1u)) continue;
       const int peer = ctx->dist_rank ^ m;
+      ctx->xbytes += (double)bytes;
       ncclResult_t r1 = ncclSend(P.buf[role], bytes, ncclUint8, peer, ctx->comm, st);
       ncclResult_t r2 = ncclRecv(P.rbuf_own[m], bytes, ncclUint8, peer, ctx->comm, st);
       if (r1 != ncclSuccess || r2 != ncclSuccess) {
@@ -841,6 +934,11 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     if (!(value == 0 || (value >= 2 && value <= 4096)))
       return fail(ctx, DSE_ERR_ARG, "coresident must be 0 or in 2..4096");
     ctx->coresident = (int)value;
+  } else if (k == "small") {  // registers of <= 9 qubits on the one-wave engine (dse_small.hip)
+    ctx->small = value != 0.0;
+  } else if (k == "small_chunk") {
+    if (!(value >= 1 && value <= 1e6)) return fail(ctx, DSE_ERR_ARG, "small_chunk must be in 1..1e6");
+    ctx->small_chunk = (int)value;
   } else if (k == "spin_limit") {  // diagnostics: partner-flag polls per hand-off (< 0: always fail)
     HIPC(set_spin_limit((int)value));
   } else if (k == "xcd_pairs") {
@@ -949,7 +1047,7 @@ int dse_add_problem_sharded(dse_ctx* ctx, int n, const double* field, const doub
   if (rc) return rc;
   if (n - shard_bits < kMinTile + 1)
     return fail(ctx, DSE_ERR_ARG, "register too small to partition");
-  if (shard_rank >= 0 && (!ctx->comm || ctx->dist_world != (1 << shard_bits) ||
+  if (shard_rank >= 0 && ((!ctx->comm && !ctx->xfn) || ctx->dist_world != (1 << shard_bits) ||
                           ctx->dist_rank != shard_rank))
     return fail(ctx, DSE_ERR_STATE, "dist shard needs dse_dist_init with world = 2^shard_bits "
                                     "and rank = shard_rank");
@@ -987,7 +1085,7 @@ int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id) {
   if (!ctx || !id) return DSE_ERR_ARG;
   if (world < 2 || world > kMaxShards || (world & (world - 1)) || rank < 0 || rank >= world)
     return fail(ctx, DSE_ERR_ARG, "world must be 2, 4 or 8 and 0 <= rank < world");
-  if (ctx->comm) return fail(ctx, DSE_ERR_STATE, "dse_dist_init called twice");
+  if (ctx->comm || ctx->xfn) return fail(ctx, DSE_ERR_STATE, "dse_dist_init called twice");
   HIPC(hipSetDevice(ctx->device));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
@@ -996,6 +1094,18 @@ int dse_dist_init(dse_ctx* ctx, int rank, int world, const unsigned char* id) {
     ctx->comm = nullptr;
     return fail(ctx, DSE_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
+  ctx->dist_rank = rank;
+  ctx->dist_world = world;
+  return DSE_OK;
+}
+
+int dse_dist_init_exchange(dse_ctx* ctx, int rank, int world, dse_exchange_fn fn, void* user) {
+  if (!ctx || !fn) return DSE_ERR_ARG;
+  if (world < 2 || world > kMaxShards || (world & (world - 1)) || rank < 0 || rank >= world)
+    return fail(ctx, DSE_ERR_ARG, "world must be 2, 4 or 8 and 0 <= rank < world");
+  if (ctx->comm || ctx->xfn) return fail(ctx, DSE_ERR_STATE, "dse_dist_init called twice");
+  ctx->xfn = fn;
+  ctx->xuser = user;
   ctx->dist_rank = rank;
   ctx->dist_world = world;
   return DSE_OK;
@@ -1072,6 +1182,192 @@ int apply_members(dse_ctx* ctx, int first, int count, hipStream_t st) {
   return DSE_OK;
 }
 
+// ---- small-register engine (dse_small.hip) ------------------------------------------------
+// Problems with P.sm: Chebyshev coefficients per distinct interval length (one output per series),
+// descriptors, then every launch of the whole evolve is enqueued on the engine's own stream
+// (ceil((n_t - 1) / small_chunk) per register size); small_gather waits for them and fills obs_out.
+int small_launch(dse_ctx* ctx, const double* t, int n_t, double tol, double* h_applications,
+                 double* launches) {
+  std::vector<int> sm;
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+    if (ctx->probs[pi].sm) sm.push_back((int)pi);
+  *h_applications = 0.0;
+  *launches = 0.0;
+  if (sm.empty()) return DSE_OK;
+  if (!ctx->small_stream) HIPC(hipStreamCreateWithFlags(&ctx->small_stream, hipStreamNonBlocking));
+  // distinct interval lengths -> sets
+  std::vector<double> taus;
+  std::vector<int> iv_set(std::max(n_t - 1, 1), 0);
+  std::map<double, int> tau_id;
+  for (int m = 0; m + 1 < n_t; ++m) {
+    const double tau = t[m + 1] - t[m];
+    auto it = tau_id.find(tau);
+    if (it == tau_id.end()) {
+      if (taus.size() >= 4096) return fail(ctx, DSE_ERR_ARG, "more than 4096 distinct output intervals");
+      it = tau_id.emplace(tau, (int)taus.size()).first;
+      taus.push_back(tau);
+    }
+    iv_set[m] = it->second;
+  }
+  if (taus.empty()) taus.push_back(0.0);
+  const int n_sets = (int)taus.size();
+  std::vector<SmallProb> desc(ctx->probs.size());
+  std::memset(desc.data(), 0, desc.size() * sizeof(SmallProb));
+  for (int pi : sm) {
+    HostProblem& P = ctx->probs[pi];
+    const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
+    const double beta = 0.5 * (P.e_max + P.e_min);
+    std::vector<std::vector<double>> J(n_sets);
+    std::vector<int> deg(n_sets, 1);
+    int kcap = 1;
+    for (int sidx = 0; sidx < n_sets; ++sidx) {
+      const double z = alpha * taus[sidx];
+      const int kmax = (int)std::ceil(z + 12.0 * std::cbrt(z + 1.0) + 60.0);
+      if (kmax > ctx->max_degree)
+        return fail(ctx, DSE_ERR_CONVERGENCE, "Chebyshev degree " + std::to_string(kmax) +
+                                                  " exceeds max_degree; use a finer output grid");
+      J[sidx].resize(kmax + 1);
+      if (dse_bessel_j(z, kmax, J[sidx].data(), tol, &deg[sidx]) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
+      kcap = std::max(kcap, deg[sidx]);
+    }
+    for (int m = 0; m + 1 < n_t; ++m) *h_applications += deg[iv_set[m]];
+    const int kcap1 = kcap + 1;
+    std::vector<double2> a((size_t)n_sets * kcap1, make_double2(0.0, 0.0));
+    for (int sidx = 0; sidx < n_sets; ++sidx) {
+      const double ph = -beta * taus[sidx];
+      const std::complex<double> e(std::cos(ph), std::sin(ph));
+      std::complex<double> mi(1.0, 0.0);
+      for (int k = 0; k <= deg[sidx]; ++k) {
+        const std::complex<double> v = e * mi * ((k == 0 ? 1.0 : 2.0) * J[sidx][k]);
+        a[(size_t)sidx * kcap1 + k] = make_double2(v.real(), v.imag());
+        mi *= std::complex<double>(0.0, -1.0);
+      }
+    }
+    const size_t cb = a.size() * sizeof(double2), db = deg.size() * sizeof(int);
+    if (cb > P.sm_coef_bytes) {
+      if (P.sm_coef) (void)hipFree(P.sm_coef), P.sm_coef = nullptr;
+      if (hipMalloc(&P.sm_coef, cb) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed");
+      P.sm_coef_bytes = cb;
+    }
+    if (db > P.sm_deg_bytes) {
+      if (P.sm_deg) (void)hipFree(P.sm_deg), P.sm_deg = nullptr;
+      if (hipMalloc(&P.sm_deg, db) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed");
+      P.sm_deg_bytes = db;
+    }
+    HIPC(hipMemcpy(P.sm_coef, a.data(), cb, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(P.sm_deg, deg.data(), db, hipMemcpyHostToDevice));
+    P.degree = kcap;
+    const DevProb& d = ctx->h_desc[pi];
+    SmallProb& q = desc[pi];
+    q.state = P.buf[0];
+    q.field = d.field;
+    q.zz = d.zz;
+    q.pair = nullptr;
+    q.flip = nullptr;
+    q.coef = P.sm_coef;
+    q.deg = P.sm_deg;
+    q.sea_mask = P.sea_mask;
+    q.shift = P.shift;
+    q.beta = beta;
+    q.s1 = 1.0 / alpha;
+    q.n = P.n;
+    q.rare_bit = P.rare_bit;
+    q.kcap1 = kcap1;
+    q.n_t = n_t;
+    P.final_bsel = 0;
+  }
+  // pair / flip tables: the problem's full n x n and 4n arrays (the device tables hold field, zz)
+  size_t extra = 0;
+  for (int pi : sm) extra += (size_t)ctx->probs[pi].n * ctx->probs[pi].n + 4 * (size_t)ctx->probs[pi].n;
+  // aux ints: per register size the selection of problems, then the interval -> set map
+  const size_t aux = ctx->probs.size() + (size_t)std::max(n_t - 1, 1) + 2 * extra + 64;
+  if (aux > ctx->small_aux_cap) {
+    if (ctx->d_small_aux) (void)hipFree(ctx->d_small_aux), ctx->d_small_aux = nullptr;
+    if (hipMalloc(&ctx->d_small_aux, aux * sizeof(int)) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "small-engine allocation failed");
+    ctx->small_aux_cap = aux;
+  }
+  // tables after the ints (8-byte aligned)
+  double* tab = reinterpret_cast<double*>(ctx->d_small_aux + ((ctx->probs.size() + std::max(n_t - 1, 1) + 1) & ~size_t(1)));
+  {
+    std::vector<double> ht;
+    ht.reserve(extra);
+    std::vector<size_t> off(ctx->probs.size(), 0);
+    for (int pi : sm) {
+      const HostProblem& P = ctx->probs[pi];
+      off[pi] = ht.size();
+      ht.insert(ht.end(), P.pair.begin(), P.pair.end());
+      // drives as the engine's kernels see them (cos(pi/2) residue dropped, build_tables)
+      for (int b = 0; b < P.n; ++b)
+        for (int c = 0; c < 4; c += 2) {
+          double re = P.flip[4 * b + c], im = P.flip[4 * b + c + 1];
+          if (std::fabs(re) <= 1e-15 * std::hypot(re, im)) re = 0.0;
+          ht.push_back(re);
+          ht.push_back(im);
+        }
+    }
+    if (!ht.empty()) HIPC(hipMemcpy(tab, ht.data(), ht.size() * sizeof(double), hipMemcpyHostToDevice));
+    for (int pi : sm) {
+      desc[pi].pair = tab + off[pi];
+      desc[pi].flip = tab + off[pi] + (size_t)ctx->probs[pi].n * ctx->probs[pi].n;
+    }
+  }
+  if (desc.size() > ctx->small_cap) {
+    if (ctx->d_small) (void)hipFree(ctx->d_small), ctx->d_small = nullptr;
+    if (hipMalloc(&ctx->d_small, desc.size() * sizeof(SmallProb)) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "small-engine allocation failed");
+    ctx->small_cap = desc.size();
+  }
+  HIPC(hipMemcpy(ctx->d_small, desc.data(), desc.size() * sizeof(SmallProb), hipMemcpyHostToDevice));
+  const size_t outn = ctx->probs.size() * (size_t)n_t * 8;
+  if (outn > ctx->small_out_cap) {
+    if (ctx->d_small_out) (void)hipFree(ctx->d_small_out), ctx->d_small_out = nullptr;
+    if (hipMalloc(&ctx->d_small_out, outn * sizeof(double)) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "small-engine output allocation failed");
+    ctx->small_out_cap = outn;
+  }
+  // selections per register size, then the interval -> set map
+  std::vector<int> ints;
+  std::vector<std::pair<int, std::pair<int, int>>> groups;  // n -> (offset, count)
+  for (int n = 1; n <= kSmallMaxQubits; ++n) {
+    const int o = (int)ints.size();
+    for (int pi : sm)
+      if (ctx->probs[pi].n == n) ints.push_back(pi);
+    if ((int)ints.size() > o) groups.push_back({n, {o, (int)ints.size() - o}});
+  }
+  const int iv_off = (int)ints.size();
+  ints.insert(ints.end(), iv_set.begin(), iv_set.end());
+  HIPC(hipMemcpy(ctx->d_small_aux, ints.data(), ints.size() * sizeof(int), hipMemcpyHostToDevice));
+  hipStream_t st = ctx->small_stream;
+  for (const auto& g : groups)
+    HIPC(launch_small_obs0(g.first, ctx->d_small, ctx->d_small_aux + g.second.first, g.second.second,
+                           ctx->d_small_out, st));
+  const int chunk = std::max(1, ctx->small_chunk);
+  for (int m0 = 0; m0 + 1 < n_t; m0 += chunk) {
+    const int cnt = std::min(chunk, n_t - 1 - m0);
+    for (const auto& g : groups) {
+      HIPC(launch_small(g.first, ctx->d_small, ctx->d_small_aux + g.second.first, g.second.second, m0,
+                        cnt, ctx->d_small_aux + iv_off, ctx->d_small_out, st));
+      *launches += 1.0;
+    }
+  }
+  return DSE_OK;
+}
+
+int small_gather(dse_ctx* ctx, int n_t, double* obs_out) {
+  bool any = false;
+  for (auto& P : ctx->probs) any = any || P.sm;
+  if (!any) return DSE_OK;
+  HIPC(hipStreamSynchronize(ctx->small_stream));
+  std::vector<double> h(ctx->probs.size() * (size_t)n_t * 8);
+  HIPC(hipMemcpy(h.data(), ctx->d_small_out, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    const HostProblem& P = ctx->probs[pi];
+    if (!P.sm) continue;
+    for (int ti = 0; ti < n_t; ++ti)
+      finish_obs(P, h.data() + (pi * (size_t)n_t + ti) * 8, obs_out + pi * DSE_N_OBS * (size_t)n_t + ti,
+                 (size_t)n_t);
+  }
+  return DSE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1134,17 +1430,7 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int64_t t = 0; t < tiles; ++t)
     for (int j = 0; j < 7; ++j) v[j] += h[t * 8 + j];
-  if (ctx->probs[first].dist) {  // sum over the shards of all ranks
-    double* d = nullptr;
-    HIPC(hipMalloc(&d, 7 * sizeof(double)));
-    HIPC(hipMemcpy(d, v, 7 * sizeof(double), hipMemcpyHostToDevice));
-    const ncclResult_t r = ncclAllReduce(d, d, 7, ncclFloat64, ncclSum, ctx->comm, st);
-    hipError_t e = hipStreamSynchronize(st);
-    if (e == hipSuccess) e = hipMemcpy(v, d, 7 * sizeof(double), hipMemcpyDeviceToHost);
-    (void)hipFree(d);
-    if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    HIPC(e);
-  }
+  if (ctx->probs[first].dist && (rc = xchg_allreduce_host(ctx, v, 7, st))) return rc;  // all shards
   finish_obs(ctx->probs[first], v, obs7, 1);
   ctx->evolved = false;
   return DSE_OK;
@@ -1163,13 +1449,23 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   HIPC(hipSetDevice(ctx->device));
   int rc = prepare(ctx);
   if (rc) return rc;
+  ctx->xbytes = 0.0;
 
   // ---- execution mode ----
-  // persistent: every problem fits one or two register-block tiles -> one k_interval launch per
-  // group of output intervals and lane.  streaming: per-term kernels, one output per group.
+  // small registers (n <= 9): the one-wave engine (dse_small.hip) on its own stream, whatever the
+  // other problems run on.  Of the rest -- persistent: every problem fits one or two
+  // register-block tiles -> one k_interval launch per group of output intervals and lane;
+  // streaming: per-term kernels, one output per group.
+  bool any_small = false, any_big = false;
+  for (auto& P : ctx->probs) {
+    P.sm = ctx->small && P.shard_bits == 0 && P.n_local <= kSmallMaxQubits;
+    any_small = any_small || P.sm;
+    any_big = any_big || !P.sm;
+  }
   bool persistent = ctx->persistent != 0;
   bool any_dist = false;
   for (auto& P : ctx->probs) {
+    if (P.sm) continue;
     if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
     any_dist = any_dist || P.dist;
   }
@@ -1191,7 +1487,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   // coarse grids (alpha dt >= 400) the saving is nil and the coefficient tables grow, so M = 1.
   double max_z = 0.0;
   for (int m = 0; m + 1 < n_t; ++m)
-    for (auto& P : ctx->probs) max_z = std::max(max_z, 0.5 * (P.e_max - P.e_min) * (t[m + 1] - t[m]));
+    for (auto& P : ctx->probs)
+      if (!P.sm) max_z = std::max(max_z, 0.5 * (P.e_max - P.e_min) * (t[m + 1] - t[m]));
   int M = 1;
   if (persistent && max_z < 400.0) M = std::max(1, std::min(ctx->outputs_per_launch, n_t - 1));
 
@@ -1227,6 +1524,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   // ---- Chebyshev coefficients per problem: rows [set][output j][term k] ----
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     HostProblem& P = ctx->probs[pi];
+    if (P.sm) continue;
     const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
     const double beta = 0.5 * (P.e_max + P.e_min);
     int deg = 1;
@@ -1297,7 +1595,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   {
     size_t need = 0;
     if (M > 1)
-      for (auto& P : ctx->probs) need += (size_t)(M - 1) << P.n_local;
+      for (auto& P : ctx->probs)
+        if (!P.sm) need += (size_t)(M - 1) << P.n_local;
     if (need > ctx->xacc_cap) {
       if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
       ctx->xacc_cap = 0;
@@ -1308,8 +1607,9 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     }
     size_t off = 0;
     for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
-      ctx->h_desc[pi].xacc = M > 1 ? ctx->d_xacc + off : nullptr;
-      if (M > 1) off += (size_t)(M - 1) << ctx->probs[pi].n_local;
+      const bool use = M > 1 && !ctx->probs[pi].sm;
+      ctx->h_desc[pi].xacc = use ? ctx->d_xacc + off : nullptr;
+      if (use) off += (size_t)(M - 1) << ctx->probs[pi].n_local;
     }
   }
 
@@ -1339,9 +1639,12 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   }
   HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
   // dist shards: one lane, so the RCCL exchanges are stream-ordered with every launch
-  const int n_lanes = any_dist ? 1 : std::min<int>(ctx->n_streams, (int)ctx->probs.size());
-  std::vector<int> order(ctx->probs.size());
-  std::iota(order.begin(), order.end(), 0);
+  int n_big = 0;
+  for (auto& P : ctx->probs) n_big += P.sm ? 0 : 1;
+  const int n_lanes = any_dist ? 1 : std::max(1, std::min<int>(ctx->n_streams, n_big));
+  std::vector<int> order;
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+    if (!ctx->probs[pi].sm) order.push_back((int)pi);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
     return ctx->probs[a].degree > ctx->probs[b].degree;
   });
@@ -1414,7 +1717,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   }
   HIPC(hipMemcpy(ctx->d_items, items.data(), items.size() * sizeof(int2), hipMemcpyHostToDevice));
   bool imag_all = true;
-  for (auto& P : ctx->probs) imag_all = imag_all && P.imag;
+  for (auto& P : ctx->probs) imag_all = imag_all && (P.sm || P.imag);
   // 2-tile interval launches go out in chunks whose workgroups can all be resident at once (the
   // pairs hand off every term): the occupancy query x compute units, even.
   int64_t pair_cap = 2;
@@ -1475,6 +1778,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     }
   }
   HIPC(hipStreamSynchronize(st0));
+  double small_happl = 0.0, small_launches = 0.0;
+  if (any_small && (rc = small_launch(ctx, t, n_t, tol, &small_happl, &small_launches))) return rc;
 
   const size_t chunk = (size_t)std::min<int64_t>(
       n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64)));
@@ -1622,7 +1927,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     for (int pool = 0; pool < 2; ++pool)
       if ((rc = drain(ctx->lanes[li], li, pool))) return rc;
   if ((rc = sync_all(ctx))) return rc;
-  if (persistent) {
+  if ((rc = small_gather(ctx, n_t, obs_out))) return rc;
+  if (persistent && any_big) {
     int herr = 0;
     HIPC(hipMemcpy(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (herr) {
@@ -1642,17 +1948,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     }
   }
   if (any_dist) {  // sums over all shards of the register, then normalisation (finish_obs)
-    double* d_raw = nullptr;
-    const size_t rb = dist_raw.size() * sizeof(double);
-    HIPC(hipMalloc(&d_raw, rb));
-    hipStream_t st = ctx->lanes[0].stream;
-    HIPC(hipMemcpyAsync(d_raw, dist_raw.data(), rb, hipMemcpyHostToDevice, st));
-    const ncclResult_t r = ncclAllReduce(d_raw, d_raw, dist_raw.size(), ncclFloat64, ncclSum, ctx->comm, st);
-    hipError_t e = hipMemcpyAsync(dist_raw.data(), d_raw, rb, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(d_raw);
-    if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    HIPC(e);
+    if ((rc = xchg_allreduce_host(ctx, dist_raw.data(), dist_raw.size(), ctx->lanes[0].stream))) return rc;
     for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
       if (!ctx->probs[pi].dist) continue;
       for (int ti = 0; ti < n_t; ++ti)
@@ -1661,11 +1957,13 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     }
   }
   ctx->last_q = n_groups & 1;
+  for (auto& P : ctx->probs) P.final_bsel = P.sm ? 0 : (ctx->last_q ? 2 : 0);
   ctx->evolved = true;
 
   if (stats) {
-    double happl = 0.0;
-    for (auto& P : ctx->probs) happl += (double)P.degree * n_groups;
+    double happl = small_happl;
+    for (auto& P : ctx->probs)
+      if (!P.sm) happl += (double)P.degree * n_groups;
     std::memset(stats, 0, sizeof(*stats));
     stats->h_applications = happl;
     stats->amplitude_updates = amp_updates;
@@ -1673,18 +1971,21 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->h_flops = all_flops;
     stats->timed_flops = flops_timed;
     stats->timed_amp_terms = amps_timed;
-    stats->mode = persistent ? 1 : (used_wht ? 2 : 0);
+    stats->mode = !any_big ? 3 : (persistent ? 1 : (used_wht ? 2 : 0));
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
-    stats->step_launches = launches;
+    stats->step_launches = launches + small_launches;
     stats->timed_launches = launches_timed;
     stats->timed_bytes = bytes_timed;
     stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+    for (auto& P : ctx->probs)
+      if (P.sm) max_deg = std::max(max_deg, P.degree);
     stats->max_degree = max_deg;
     stats->n_intervals = n_t - 1;
     stats->tile_bits = ctx->probs.empty() ? 0 : ctx->probs.front().L;
     stats->streams = n_lanes;
     stats->outputs_per_launch = M;
     stats->handoff_fallbacks = ctx->handoff_fallbacks;
+    stats->exchange_bytes = ctx->xbytes;
   }
   return DSE_OK;
 }
@@ -1698,12 +1999,11 @@ int dse_get_state(dse_ctx* ctx, int problem, double* psi_out) {
   int first = 0, count = 1;
   int rc = hook_members(ctx, problem, &first, &count);
   if (rc) return rc;
-  const int bsel = ctx->last_q ? 2 : 0;
   double2* out = reinterpret_cast<double2*>(psi_out);
   for (int i = 0; i < count; ++i) {
     HostProblem& P = ctx->probs[first + i];
     const size_t amps = size_t(1) << P.n_local;
-    HIPC(hipMemcpy(out + i * amps, P.buf[bsel], amps * sizeof(double2), hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(out + i * amps, P.buf[P.final_bsel], amps * sizeof(double2), hipMemcpyDeviceToHost));
   }
   return DSE_OK;
 }
@@ -1718,11 +2018,10 @@ int dse_energy(dse_ctx* ctx, int problem, double* e_out) {
   if (ctx->probs[first].dist) return fail(ctx, DSE_ERR_ARG, "dse_energy: not available for a dist shard");
   HIPC(hipSetDevice(ctx->device));
   hipStream_t st = ctx->lanes[0].stream;
-  const int bsel = ctx->last_q ? 2 : 0;
-  for (int i = 0; i < count; ++i) {  // H reads buf[0]: copy the state there (it stays in buf[bsel])
+  for (int i = 0; i < count; ++i) {  // H reads buf[0]: copy the state there (it stays in its buffer)
     HostProblem& P = ctx->probs[first + i];
-    if (bsel != 0)
-      HIPC(hipMemcpyAsync(P.buf[0], P.buf[bsel], (size_t(1) << P.n_local) * sizeof(double2),
+    if (P.final_bsel != 0)
+      HIPC(hipMemcpyAsync(P.buf[0], P.buf[P.final_bsel], (size_t(1) << P.n_local) * sizeof(double2),
                           hipMemcpyDeviceToDevice, st));
   }
   if ((rc = apply_members(ctx, first, count, st))) return rc;

@@ -148,6 +148,37 @@ class Engine:
             raise ValueError("unique id must have DSE_DIST_ID_BYTES bytes")
         self._check(self._L.dse_dist_init(self._h, int(rank), int(world), uid))
 
+    def dist_init_exchange(self, rank: int, world: int, dist) -> None:
+        """Join a partitioned register's ranks over ``dist`` (an initialised torch.distributed,
+        e.g. gloo) instead of RCCL: libdse hands every exchange to this host callback
+        (include/dse.h dse_dist_init_exchange)."""
+        import torch
+
+        def view(addr, nbytes, dtype):
+            buf = (C.c_uint8 * nbytes).from_address(addr)
+            return torch.from_numpy(np.frombuffer(buf, dtype=dtype))
+
+        def fn(_user, op, send, recv, nbytes, peer):
+            try:
+                if op == _lib.DSE_XCHG_ALLTOALL:
+                    dist.all_to_all_single(view(recv, nbytes * world, np.uint8),
+                                           view(send, nbytes * world, np.uint8))
+                elif op == _lib.DSE_XCHG_SENDRECV:
+                    reqs = [dist.isend(view(send, nbytes, np.uint8), peer),
+                            dist.irecv(view(recv, nbytes, np.uint8), peer)]
+                    for r in reqs:
+                        r.wait()
+                elif op == _lib.DSE_XCHG_ALLREDUCE_F64:
+                    dist.all_reduce(view(send, nbytes, np.float64))
+                else:
+                    return 1
+                return 0
+            except Exception:  # reported to the library as a failed exchange
+                return 1
+
+        self._xfn = _lib.EXCHANGE_FN(fn)   # kept alive with the engine
+        self._check(self._L.dse_dist_init_exchange(self._h, int(rank), int(world), self._xfn, None))
+
     def clear(self) -> None:
         self._check(self._L.dse_clear(self._h))
         self.problems = []
