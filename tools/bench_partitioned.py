@@ -89,6 +89,9 @@ def main():
     shard_bytes = (1 << (n - bits)) * 16
     wht = st.get("mode") == 2
     xbytes = 4 * shard_bytes * (shards - 1) // shards if wht else n_masks * shard_bytes
+    measured = st.get("exchange_bytes", 0.0)   # libdse's count of this rank's off-device bytes
+    happ = max(st["h_applications"], 1)
+    links = max(shards - 1, 1)                 # fully connected xGMI: one link per peer
     if rank == 0:
         print(json.dumps({
             "config": f"config 5: N={n} center_on delta={a.delta:g} Hz, t_final={a.t_final}, "
@@ -98,6 +101,11 @@ def main():
             "shard_GiB": shard_bytes / 2**30, "engine_mode": st.get("mode"),
             "exchange": "index-swap all-to-all of A, B (x2)" if wht else f"send/recv, {n_masks} partner masks",
             "exchange_bytes_per_h_per_rank": xbytes,
+            "exchange_bytes_measured_per_rank": measured,
+            "exchange_bytes_measured_per_h_per_rank": measured / happ,
+            # the exchange's bytes per link over the whole call's wall time: a lower bound of the
+            # per-link rate while the exchange runs (the passes run between exchanges)
+            "xgmi_gbs_per_link_lower_bound": (measured / links / wall / 1e9) if not a.loopback else None,
             "obs_t_final": obs_d,
         }), flush=True)
 
