@@ -20,7 +20,10 @@ __host__ __device__ constexpr int rr_index(int a, int b) {
   return a * (2 * kRegBits - a - 1) / 2 + (b - a - 1);
 }
 constexpr int kXSlots = 4;                        // hand-off ring of the interval kernel
-constexpr int kMaxOut = 2;                        // output times per interval-kernel launch
+#ifndef DSE_MAX_OUT
+#define DSE_MAX_OUT 2
+#endif
+constexpr int kMaxOut = DSE_MAX_OUT;              // output times per interval-kernel launch
 constexpr int kMaxShardBits = 3;                  // partitioned registers: up to 8 shards
 constexpr int kMaxShards = 1 << kMaxShardBits;
 // bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index

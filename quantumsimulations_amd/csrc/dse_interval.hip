@@ -439,7 +439,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         out[r].y = fma(2.0 * s1, out[r].y, -prev[r].y);
       }
     }
-    constexpr int AB = 4;
+    constexpr int AB = kMaxOut <= 2 ? 4 : (kMaxOut == 3 ? 2 : 1);  // VGPR budget: AB x kMaxOut loads
     const int nj = (ab & 256) ? 0 : n_out;
     bool upd[kMaxOut];
     __amdgpu_buffer_rsrc_t acc_j[kMaxOut];

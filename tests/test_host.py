@@ -305,3 +305,22 @@ def test_wht_pass_plans_transform_every_bit_once(wl, shard_bits):
                 # every local bit once before the swap or in MID (T positions count twice: they
                 # are the leaving local bits before and the arriving shard bits in MID)
                 assert sorted(pre + [b for b in mid if b not in top]) == list(range(wl, n_local))
+
+
+def test_run_reference_launcher_resolves_the_drop_in(tmp_path):
+    """An unmodified caller placed next to a (QuTiP-importing) dipolar_ensemble_with_rare.py, as the
+    reference's sweep_sea_detuning.py is, picks up the MI355X drop-in under the launcher."""
+    import subprocess
+    import sys
+    (tmp_path / "dipolar_ensemble_with_rare.py").write_text("import qutip  # the reference's module\n")
+    (tmp_path / "caller.py").write_text(
+        "from dipolar_ensemble_with_rare import DipolarRareParams, simulate_rare, "
+        "get_derived_frequencies, shell_positions_with_rare_center, dipolar_couplings_from_positions\n"
+        "import dipolar_ensemble_with_rare as m, sys\nprint(m.simulate_rare.__module__, sys.argv[1:])\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-m", "quantumsimulations_amd.run_reference",
+                          str(tmp_path / "caller.py"), "--x", "1"], cwd=root, capture_output=True,
+                         text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert res.stdout.split()[0] == "quantumsimulations_amd.dipolar_ensemble_with_rare"
+    assert "'--x', '1'" in res.stdout
