@@ -49,6 +49,7 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None) ->
     tmp = target + ".tmp"
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
              "-Wno-unused-function", "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
+    flags += os.environ.get("DSE_EXTRA_FLAGS", "").split()  # e.g. -DDSE_ACC_BLOCK=2 for a variant library
     with tempfile.TemporaryDirectory(prefix="dse_build_") as tdir:
         objs = [os.path.join(tdir, s + ".o") for s in SOURCES]
         cmds = [[hipcc, *flags, "-c", os.path.join(CSRC, s), "-o", o] for s, o in zip(SOURCES, objs)]
