@@ -76,7 +76,7 @@ struct DevProb {
   const DFlip* flips_hi;  // both kernels
   const DSweep* sweeps;   // register-block kernel: [L-kRegBits] thread-bit sweeps
   const DPair* pairs_tt;  // register-block kernel: pairs between two thread bits
-  const CoefK* coef;      // [n_sets][kcap1] Chebyshev coefficients per term
+  const double2* coef;    // compact Chebyshev rows, see coef_row / coef_at
   uint64_t sea_mask;
   double shift;
   double beta;            // spectral centre
@@ -100,11 +100,37 @@ struct DevProb {
   double2* xslots;        // interval kernel, 2-tile problems: [2][kXSlots][2^L] hand-off slots
   // Multi-output launches: one interval-kernel launch propagates n_out <= n_acc consecutive output
   // times from a shared Chebyshev series.  Output j < n_out - 1 is accumulated in
-  // xacc[j << n_local], the last in the next psi buffer.  Coefficient rows: coef[(set * n_acc + j)
-  // * kcap1 + k].
+  // xacc[j << n_local], the last in the next psi buffer.
   double2* xacc;
   int n_acc;
 };
+
+// Coefficient row of output j of offset set `set`: kcap1 + 1 entries, row[0].x = the degree d of
+// that output's series, row[1 + k] = a_k for k = 0..d (zero beyond): 16 B per term.
+__host__ __device__ __forceinline__ const double2* coef_row(const DevProb& P, int set, int j) {
+  return P.coef + ((size_t)set * P.n_acc + j) * (size_t)(P.kcap1 + 1);
+}
+// Terms accumulated at term k (see CoefK): 2 at k = 1 (a_0 w_0 + a_1 w_1), 3 every third term
+// (k - 1 = 0 mod 3: a_{k-2}, a_{k-1}, a_k), the r = (k - 1) mod 3 left over at k = d, else 0.
+__host__ __device__ __forceinline__ int coef_nterm(int k, int d) {
+  if (k > d) return 0;
+  if (k == 1) return 2;
+  const int r = (k - 1) % 3;
+  return r == 0 ? 3 : (k == d ? r : 0);
+}
+// (scalar loads: the row is read-only during a launch and uniform across the workgroup)
+__device__ __forceinline__ CoefK coef_at(const double2* row, int k) {
+  typedef const __attribute__((address_space(4))) double* kptr;
+  const kptr r = (kptr)row;
+  const int nt = coef_nterm(k, (int)r[0]);
+  CoefK C = {};
+  C.upd = nt > 0;
+  const size_t o = 2 * (size_t)(k - 1);  // a_{k-2} at row[k - 1]
+  C.c[0] = nt >= 3 ? make_double2(r[o], r[o + 1]) : make_double2(0.0, 0.0);
+  C.c[1] = nt >= 2 ? make_double2(r[o + 2], r[o + 3]) : make_double2(0.0, 0.0);
+  C.c[2] = nt >= 1 ? make_double2(r[o + 4], r[o + 5]) : make_double2(0.0, 0.0);
+  return C;
+}
 
 // Global tile hp of the role-`role` vector: local buffer or a partner shard's.
 __device__ __forceinline__ const double2* tile_ptr(const DevProb& P, int role, uint32_t hp) {
@@ -126,8 +152,18 @@ hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* i
                            int set, int n_out, int* flags, int* err, hipStream_t st);
 // zeroes the interval kernel's hand-off flags of the given items (before a 2-tile launch)
 hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st);
+// psi(t0) of many registers in one launch: entry i zeroes ptr[0 .. n) and sets ptr[one_at] = 1
+// (one_at < 0: the basis state lies in another shard)
+struct BasisInit {
+  double2* ptr;
+  uint64_t n;
+  int64_t one_at;
+};
+hipError_t launch_basis_init(const BasisInit* list, int n_entries, uint64_t max_amps, hipStream_t st);
+// observables of n_out outputs of a group (grid.y): output j < n_out - 1 from intermediate
+// accumulator j, the last from state buffer role bsel; output j's partials at partial + j * out_stride
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
-                      double* partial, hipStream_t st);
+                      double* partial, hipStream_t st, int n_out = 1, size_t out_stride = 0);
 // partial[2 * block + {0, 1}] = block sums of Re(conj(a) b) and |a|^2 over n amplitudes
 hipError_t launch_dot(const double2* a, const double2* b, size_t n, double* partial, int blocks,
                       hipStream_t st);

@@ -146,7 +146,14 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const cptr<DPair> ctt = cst(P.pairs_tt);
   const cptr<DPair> cph = cst(P.pairs_hi);
   const cptr<DFlip> cfh = cst(P.flips_hi);
-  const cptr<CoefK> ccoef = cst(P.coef + (size_t)set * P.n_acc * P.kcap1);  // [j][k] rows
+  // coefficient rows of the outputs (coef_row): [j][0].x = degree d_j, [j][1 + k] = a_k
+  // (vector loads of uniform addresses: the scalar-load form of these reads, measured, made the
+  // 2-tile problems' results vary from run to run at the 1e-10 level; tools/diag_repeat.py)
+  const double* crow = (const double*)coef_row(P, set, 0);
+  const size_t rstride = 2 * (size_t)(P.kcap1 + 1);  // doubles per row
+  int dj[kMaxOut];
+#pragma unroll
+  for (int j = 0; j < kMaxOut; ++j) dj[j] = j < n_out ? (int)crow[j * rstride] : 0;
   const int n_tt = P.n_pairs_tt;
   // the top-bit drive (cross flip) for this tile's output bit value (raw exchange)
   double xr = 0.0, xi = 0.0;
@@ -445,7 +452,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
     __amdgpu_buffer_rsrc_t acc_j[kMaxOut];
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
-      upd[j] = j < nj && ccoef[(size_t)j * P.kcap1 + k].upd;
+      upd[j] = j < nj && coef_nterm(k, dj[j]) > 0;
       acc_j[j] = (j == n_out - 1) ? acc_t
                                   : tile_rsrc(P.xacc + ((size_t)j << (L + P.tbl)) + (h << L), TBYTES);
     }
@@ -464,8 +471,10 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
       for (int j = 0; j < kMaxOut; ++j) {
         if (!upd[j]) continue;
-        const cptr<double> cc = (cptr<double>)(ccoef + (size_t)j * P.kcap1 + k);  // c[0..2] (re, im)
-        const double2 c0 = make_double2(cc[0], cc[1]), c1 = make_double2(cc[2], cc[3]),
+        const int nt = coef_nterm(k, dj[j]);
+        const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);  // a_{k-2}, a_{k-1}, a_k
+        const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
+                      c1 = nt >= 2 ? make_double2(cc[2], cc[3]) : make_double2(0.0, 0.0),
                       c2 = make_double2(cc[4], cc[5]);
 #pragma unroll
         for (int r = 0; r < AB; ++r) {

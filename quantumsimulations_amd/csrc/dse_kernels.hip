@@ -12,6 +12,8 @@
 // MODE_APPLY: out = H w (test hook)      MODE_FIRST: w1 = Ht w0,  acc = a0 w0 + a1 w1
 // MODE_GEN:   w_k = 2 Ht w_{k-1} - w_{k-2} (in place over w_{k-2}),  acc += a_k w_k
 // with Ht = (H - beta) / alpha.
+#include <algorithm>
+
 #include "dse_device.h"
 
 namespace dse {
@@ -151,7 +153,7 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
 
   // ---- recurrence + accumulation ----
   CoefK C = {};
-  if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
+  if (MODE != MODE_APPLY) C = coef_at(coef_row(P, set, 0), MODE == MODE_FIRST ? 1 : k);
   const double scale = MODE == MODE_GEN ? 2.0 * P.s1 : P.s1;
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -163,8 +165,8 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
 // <Ix_k> = sum_{bit_k(x)=0} Re(conj(psi_x) psi_{x^e_k}),  <Iy_k> = Im(...),  <Iz_k> = sum |psi_x|^2 s_k(x)
 template <int L>
 __global__ void __launch_bounds__(Geo<L>::NT)
-k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bsel,
-      double* __restrict__ partial) {
+k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bsel_last,
+      double* __restrict__ partial, size_t out_stride) {
   using G = Geo<L>;
   constexpr int T = G::T, NT = G::NT, R = G::R;
   __shared__ double2 s_w[T];
@@ -176,7 +178,10 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
   const uint32_t hg = P.h_base | h;
   const int tid = threadIdx.x;
   const bool live = (T >= NT) || (tid < T);
-  // bsel < 3: a state buffer role; bsel = 3 + j: intermediate output j of a multi-output launch
+  // blockIdx.y = output j of the group: the last one in state buffer role bsel_last (< 3), the
+  // others in intermediate output j (bsel = 3 + j) of a multi-output launch
+  const int bsel = (blockIdx.y == gridDim.y - 1) ? bsel_last : 3 + (int)blockIdx.y;
+  partial += (size_t)blockIdx.y * out_stride;
   const double2* psi = bsel < 3 ? P.buf[bsel] : P.xacc + ((size_t)(bsel - 3) << (L + P.tbl));
   const size_t base = (size_t)h << L;
 
@@ -335,7 +340,7 @@ k_step_rb(const DevProb* __restrict__ probs, const int2* __restrict__ items, int
   }
   // epilogue operand w_{k-2}: issued now, its latency hides under the thread-pair loop
   CoefK C = {};
-  if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
+  if (MODE != MODE_APPLY) C = coef_at(coef_row(P, set, 0), MODE == MODE_FIRST ? 1 : k);
   const bool rd = (MODE == MODE_GEN) && !(ab & 8);
   double2 prev[R];
   if (rd) {
@@ -448,8 +453,9 @@ hipError_t launch_step_L(int mode, const DevProb* probs, const int2* items, int 
 
 template <int L>
 hipError_t launch_obs_L(const DevProb* probs, const int2* items, int n_items, int bsel,
-                        double* partial, hipStream_t st) {
-  hipLaunchKernelGGL((k_obs<L>), dim3(n_items), dim3(Geo<L>::NT), 0, st, probs, items, bsel, partial);
+                        double* partial, hipStream_t st, int n_out, size_t out_stride) {
+  hipLaunchKernelGGL((k_obs<L>), dim3(n_items, n_out), dim3(Geo<L>::NT), 0, st, probs, items, bsel,
+                     partial, out_stride);
   return hipGetLastError();
 }
 
@@ -499,15 +505,32 @@ hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items,
 }
 
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
-                      double* partial, hipStream_t st) {
-  if (n_items <= 0) return hipSuccess;
+                      double* partial, hipStream_t st, int n_out, size_t out_stride) {
+  if (n_items <= 0 || n_out <= 0) return hipSuccess;
+  if (n_out > 1 && bsel >= 3) return hipErrorInvalidValue;
   switch (L) {
 #define X(l) \
-  case l: return launch_obs_L<l>(probs, items, n_items, bsel, partial, st);
+  case l: return launch_obs_L<l>(probs, items, n_items, bsel, partial, st, n_out, out_stride);
     DSE_TILE_CASES(X)
 #undef X
     default: return hipErrorInvalidValue;
   }
+}
+
+// one basis state per register: grid.y = entry, grid-stride over its amplitudes (16-B stores)
+__global__ void __launch_bounds__(256) k_basis_init(const BasisInit* __restrict__ list) {
+  const BasisInit e = list[blockIdx.y];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e.n; i += stride)
+    e.ptr[i] = make_double2((int64_t)i == e.one_at ? 1.0 : 0.0, 0.0);
+}
+
+hipError_t launch_basis_init(const BasisInit* list, int n_entries, uint64_t max_amps, hipStream_t st) {
+  if (n_entries <= 0) return hipSuccess;
+  if (n_entries > 65535) return hipErrorInvalidValue;
+  const uint64_t blocks = std::min<uint64_t>((max_amps + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_basis_init, dim3((unsigned)std::max<uint64_t>(blocks, 1), n_entries), dim3(256), 0, st, list);
+  return hipGetLastError();
 }
 
 hipError_t launch_dot(const double2* a, const double2* b, size_t n, double* partial, int blocks,

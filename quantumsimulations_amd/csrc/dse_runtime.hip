@@ -19,10 +19,12 @@
 #include <complex>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -49,8 +51,7 @@ struct HostProblem {
   int64_t n_tiles = 0;
   double2* buf[3] = {nullptr, nullptr, nullptr};
   void* tables = nullptr;
-  CoefK* coef = nullptr;
-  size_t coef_bytes = 0;
+  double2* coef = nullptr;   // into dse_ctx::d_coef (compact rows, coef_row)
   int degree = 1;
   double flops_per_amp = 0.0;  // algorithmic flops of one H application per amplitude
   int2* d_items = nullptr;  // this problem's tiles (apply_h / observables hooks)
@@ -69,9 +70,8 @@ struct HostProblem {
   int wht_groups = 0;        // passes' tile-bit groups; 0: this problem uses the step kernels
   // small-register engine (dse_small.hip): n <= 9 qubits, whole evolution one wave per problem
   bool sm = false;           // this evolve runs the problem on that engine
-  double2* sm_coef = nullptr;
+  double2* sm_coef = nullptr;  // into dse_ctx::d_sm_coef
   int* sm_deg = nullptr;
-  size_t sm_coef_bytes = 0, sm_deg_bytes = 0;
   int final_bsel = 0;        // buffer holding the final state after dse_evolve
 };
 
@@ -132,6 +132,13 @@ struct dse_ctx {
   size_t xslot_cap = 0;             // in amplitudes
   double2* d_xacc = nullptr;        // intermediate outputs of multi-output launches
   size_t xacc_cap = 0;              // in amplitudes
+  // per-evolve uploads, one device arena each (one copy per evolve, not one per problem)
+  unsigned char* d_coef = nullptr;  // Chebyshev coefficient rows of every problem
+  size_t coef_cap = 0;
+  unsigned char* d_sm_coef = nullptr;  // small-engine coefficients and degrees
+  size_t sm_coef_cap = 0;
+  BasisInit* d_init = nullptr;      // psi(t0) list
+  size_t init_cap = 0;
   int outputs_per_launch = 2;       // M of the interval kernel (dse_evolve picks 1 on coarse grids)
   int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
@@ -145,6 +152,7 @@ struct dse_ctx {
   std::vector<unsigned char> xsend, xrecv;
   double xbytes = 0.0;              // bytes this rank sent to other ranks (current evolve)
   // small-register engine
+  int dbg = 0;                      // diagnostics switches (option "dbg")
   int small = 1;                    // registers of <= 9 qubits run on dse_small.hip
   int small_chunk = 64;             // output intervals per launch of that engine
   hipStream_t small_stream = nullptr;
@@ -174,6 +182,54 @@ int fail(dse_ctx* c, int code, const std::string& msg) {
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// f(i) for i < n on up to 16 host threads (contiguous blocks; f must touch only item i's data).
+template <class F>
+void parallel_for(size_t n, F&& f) {
+  const size_t nth = std::min<size_t>({(size_t)std::max(1u, std::thread::hardware_concurrency()), 16, (n + 7) / 8});
+  if (nth <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nth);
+  for (size_t w = 0; w < nth; ++w)
+    th.emplace_back([&, w] {
+      for (size_t i = n * w / nth; i < n * (w + 1) / nth; ++i) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+// Host bytes gathered for one upload: pieces 64-B aligned, offsets into the device arena.
+struct Arena {
+  std::vector<unsigned char> host;
+  size_t add(const void* src, size_t bytes) {
+    const size_t off = place(bytes);
+    if (bytes) std::memcpy(host.data() + off, src, bytes);
+    return off;
+  }
+  size_t place(size_t bytes) {  // room for a piece filled later
+    const size_t off = align_up(host.size(), 64);
+    host.resize(off + bytes);
+    return off;
+  }
+};
+
+// The arena's device copy: grows *dev to fit, then one copy on stream st (stream-ordered before
+// every later launch on st; the caller synchronises st before other streams use it).
+int upload_arena(dse_ctx* ctx, const Arena& a, unsigned char** dev, size_t* cap, hipStream_t st) {
+  if (a.host.empty()) return DSE_OK;
+  if (a.host.size() > *cap) {
+    if (*dev) (void)hipFree(*dev), *dev = nullptr;
+    *cap = 0;
+    if (hipMalloc(dev, a.host.size()) != hipSuccess)
+      return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed (" + std::to_string(a.host.size()) + " bytes)");
+    *cap = a.host.size();
+  }
+  HIPC(hipMemcpyAsync(*dev, a.host.data(), a.host.size(), hipMemcpyHostToDevice, st));
+  HIPC(hipStreamSynchronize(st));  // the host bytes may be released after return
+  return DSE_OK;
+}
+
 void free_wht(HostProblem& p) {
   for (auto& b : p.wvec)
     if (b) (void)hipFree(b), b = nullptr;
@@ -187,15 +243,13 @@ void free_device(dse_ctx* ctx) {
     for (auto& b : p.buf)
       if (b) (void)hipFree(b), b = nullptr;
     if (p.tables) (void)hipFree(p.tables), p.tables = nullptr;
-    if (p.coef) (void)hipFree(p.coef), p.coef = nullptr;
+    p.coef = nullptr;
     if (p.d_items) (void)hipFree(p.d_items), p.d_items = nullptr;
     for (auto& b : p.rbuf_own)
       if (b) (void)hipFree(b), b = nullptr;
-    if (p.sm_coef) (void)hipFree(p.sm_coef), p.sm_coef = nullptr;
-    if (p.sm_deg) (void)hipFree(p.sm_deg), p.sm_deg = nullptr;
-    p.sm_coef_bytes = p.sm_deg_bytes = 0;
+    p.sm_coef = nullptr;
+    p.sm_deg = nullptr;
     free_wht(p);
-    p.coef_bytes = 0;
   }
   if (ctx->d_wht) (void)hipFree(ctx->d_wht), ctx->d_wht = nullptr;
   ctx->wht_ready = false;
@@ -210,6 +264,10 @@ void free_device(dse_ctx* ctx) {
   ctx->xslot_cap = 0;
   if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
   ctx->xacc_cap = 0;
+  if (ctx->d_coef) (void)hipFree(ctx->d_coef), ctx->d_coef = nullptr;
+  if (ctx->d_sm_coef) (void)hipFree(ctx->d_sm_coef), ctx->d_sm_coef = nullptr;
+  if (ctx->d_init) (void)hipFree(ctx->d_init), ctx->d_init = nullptr;
+  ctx->coef_cap = ctx->sm_coef_cap = ctx->init_cap = 0;
   if (ctx->d_small) (void)hipFree(ctx->d_small), ctx->d_small = nullptr;
   if (ctx->d_small_out) (void)hipFree(ctx->d_small_out), ctx->d_small_out = nullptr;
   if (ctx->d_small_aux) (void)hipFree(ctx->d_small_aux), ctx->d_small_aux = nullptr;
@@ -934,6 +992,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     if (!(value == 0 || (value >= 2 && value <= 4096)))
       return fail(ctx, DSE_ERR_ARG, "coresident must be 0 or in 2..4096");
     ctx->coresident = (int)value;
+  } else if (k == "dbg") {  // diagnostics bit mask: 1 one observable launch per output, 2 psi0 by
+                            // memset/copy, 4 coefficient tables on one host thread
+    ctx->dbg = (int)value;
   } else if (k == "small") {  // registers of <= 9 qubits on the one-wave engine (dse_small.hip)
     ctx->small = value != 0.0;
   } else if (k == "small_chunk") {
@@ -1213,6 +1274,8 @@ int small_launch(dse_ctx* ctx, const double* t, int n_t, double tol, double* h_a
   const int n_sets = (int)taus.size();
   std::vector<SmallProb> desc(ctx->probs.size());
   std::memset(desc.data(), 0, desc.size() * sizeof(SmallProb));
+  Arena arena;  // every problem's coefficients and degrees, one upload
+  std::vector<std::pair<size_t, size_t>> aoff(ctx->probs.size());
   for (int pi : sm) {
     HostProblem& P = ctx->probs[pi];
     const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
@@ -1243,19 +1306,8 @@ int small_launch(dse_ctx* ctx, const double* t, int n_t, double tol, double* h_a
         mi *= std::complex<double>(0.0, -1.0);
       }
     }
-    const size_t cb = a.size() * sizeof(double2), db = deg.size() * sizeof(int);
-    if (cb > P.sm_coef_bytes) {
-      if (P.sm_coef) (void)hipFree(P.sm_coef), P.sm_coef = nullptr;
-      if (hipMalloc(&P.sm_coef, cb) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed");
-      P.sm_coef_bytes = cb;
-    }
-    if (db > P.sm_deg_bytes) {
-      if (P.sm_deg) (void)hipFree(P.sm_deg), P.sm_deg = nullptr;
-      if (hipMalloc(&P.sm_deg, db) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed");
-      P.sm_deg_bytes = db;
-    }
-    HIPC(hipMemcpy(P.sm_coef, a.data(), cb, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(P.sm_deg, deg.data(), db, hipMemcpyHostToDevice));
+    aoff[pi].first = arena.add(a.data(), a.size() * sizeof(double2));
+    aoff[pi].second = arena.add(deg.data(), deg.size() * sizeof(int));
     P.degree = kcap;
     const DevProb& d = ctx->h_desc[pi];
     SmallProb& q = desc[pi];
@@ -1264,8 +1316,6 @@ int small_launch(dse_ctx* ctx, const double* t, int n_t, double tol, double* h_a
     q.zz = d.zz;
     q.pair = nullptr;
     q.flip = nullptr;
-    q.coef = P.sm_coef;
-    q.deg = P.sm_deg;
     q.sea_mask = P.sea_mask;
     q.shift = P.shift;
     q.beta = beta;
@@ -1275,6 +1325,17 @@ int small_launch(dse_ctx* ctx, const double* t, int n_t, double tol, double* h_a
     q.kcap1 = kcap1;
     q.n_t = n_t;
     P.final_bsel = 0;
+  }
+  {
+    int rc = upload_arena(ctx, arena, &ctx->d_sm_coef, &ctx->sm_coef_cap, ctx->small_stream);
+    if (rc) return rc;
+  }
+  for (int pi : sm) {
+    HostProblem& P = ctx->probs[pi];
+    P.sm_coef = reinterpret_cast<double2*>(ctx->d_sm_coef + aoff[pi].first);
+    P.sm_deg = reinterpret_cast<int*>(ctx->d_sm_coef + aoff[pi].second);
+    desc[pi].coef = P.sm_coef;
+    desc[pi].deg = P.sm_deg;
   }
   // pair / flip tables: the problem's full n x n and 4n arrays (the device tables hold field, zz)
   size_t extra = 0;
@@ -1439,6 +1500,16 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
 int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
   if (!ctx) return DSE_ERR_ARG;
   const auto wall0 = std::chrono::steady_clock::now();
+  // DSE_HOST_TIMING=1: host time of each phase of this call on stderr (diagnostics)
+  static const bool host_timing = std::getenv("DSE_HOST_TIMING") != nullptr;
+  auto tmark = wall0;
+  auto phase = [&](const char* name) {
+    if (!host_timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[dse_evolve] %-12s %9.3f ms\n", name,
+                 std::chrono::duration<double, std::milli>(now - tmark).count());
+    tmark = now;
+  };
   if (!t || !obs_out) return fail(ctx, DSE_ERR_ARG, "null pointer");
   if (n_t < 1) return fail(ctx, DSE_ERR_ARG, "n_t must be >= 1");
   if (!(tol > 0.0 && tol < 1e-2)) return fail(ctx, DSE_ERR_ARG, "tol must be in (0, 1e-2)");
@@ -1451,6 +1522,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   if (rc) return rc;
   ctx->xbytes = 0.0;
 
+  phase("prepare");
   // ---- execution mode ----
   // small registers (n <= 9): the one-wave engine (dse_small.hip) on its own stream, whatever the
   // other problems run on.  Of the rest -- persistent: every problem fits one or two
@@ -1521,10 +1593,17 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   const int n_sets = (int)set_tau.size();
   const int n_groups = (int)groups.size();
 
-  // ---- Chebyshev coefficients per problem: rows [set][output j][term k] ----
-  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+  phase("groups");
+  // ---- Chebyshev coefficients per problem: rows [set][output j][term k], all problems' rows
+  // gathered into one arena and uploaded with one copy ----
+  // Problems are independent: computed on up to 16 host threads (Bessel series of every distinct
+  // offset set, ~3 us each), then gathered in problem order.
+  std::vector<std::vector<double2>> coef_rows(ctx->probs.size());
+  std::vector<int> coef_rc(ctx->probs.size(), DSE_OK);
+  std::vector<std::string> coef_msg(ctx->probs.size());
+  auto coef_one = [&](size_t pi) {
     HostProblem& P = ctx->probs[pi];
-    if (P.sm) continue;
+    if (P.sm) return;
     const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
     const double beta = 0.5 * (P.e_max + P.e_min);
     int deg = 1;
@@ -1534,21 +1613,27 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       for (size_t j = 0; j < set_tau[s].size(); ++j) {
         const double z = alpha * set_tau[s][j];
         const int kmax = (int)std::ceil(z + 12.0 * std::cbrt(z + 1.0) + 60.0);
-        if (kmax > ctx->max_degree)
-          return fail(ctx, DSE_ERR_CONVERGENCE, "Chebyshev degree " + std::to_string(kmax) +
-                                                    " exceeds max_degree; use a finer output grid");
+        if (kmax > ctx->max_degree) {
+          coef_rc[pi] = DSE_ERR_CONVERGENCE;
+          coef_msg[pi] = "Chebyshev degree " + std::to_string(kmax) + " exceeds max_degree; use a finer output grid";
+          return;
+        }
         std::vector<double>& Jv = J[(size_t)s * M + j];
         Jv.resize(kmax + 1);
         int d = 1;
-        if (dse_bessel_j(z, kmax, Jv.data(), tol, &d) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
+        if (dse_bessel_j(z, kmax, Jv.data(), tol, &d) != DSE_OK) {
+          coef_rc[pi] = DSE_ERR_ARG;
+          coef_msg[pi] = "bessel failed";
+          return;
+        }
         deg_sj[(size_t)s * M + j] = d;
         deg = std::max(deg, d);
       }
     P.degree = deg;
     const int kcap1 = deg + 1;
-    std::vector<CoefK> coef((size_t)n_sets * M * kcap1);
-    std::memset(coef.data(), 0, coef.size() * sizeof(CoefK));
-    std::vector<std::complex<double>> a(deg + 1);
+    // compact rows (coef_row): [set][j] x (kcap1 + 1) entries, [0].x = degree, [1 + k] = a_k
+    std::vector<double2>& coef = coef_rows[pi];
+    coef.assign((size_t)n_sets * M * (kcap1 + 1), make_double2(0.0, 0.0));
     for (int s = 0; s < n_sets; ++s)
       for (size_t j = 0; j < set_tau[s].size(); ++j) {
         const std::vector<double>& Jv = J[(size_t)s * M + j];
@@ -1556,41 +1641,50 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         const double ph = -beta * set_tau[s][j];
         const std::complex<double> e(std::cos(ph), std::sin(ph));
         std::complex<double> mi(1.0, 0.0);  // (-i)^k
-        for (int k = 0; k <= deg; ++k) {
-          const double jk = (k <= dj && k < (int)Jv.size()) ? Jv[k] : 0.0;
-          a[k] = e * mi * ((k == 0 ? 1.0 : 2.0) * jk);
+        double2* row = coef.data() + ((size_t)s * M + j) * (kcap1 + 1);
+        row[0] = make_double2((double)dj, 0.0);
+        for (int k = 0; k <= dj; ++k) {
+          const std::complex<double> a = e * mi * ((k == 0 ? 1.0 : 2.0) * Jv[k]);
+          row[1 + k] = make_double2(a.real(), a.imag());
           mi *= std::complex<double>(0.0, -1.0);
         }
-        auto put = [](double2& d, std::complex<double> v) { d = make_double2(v.real(), v.imag()); };
-        CoefK* row = coef.data() + ((size_t)s * M + j) * kcap1;
-        put(row[1].c[1], a[0]);  // k = 1: acc = a0 w0 + a1 w1
-        put(row[1].c[2], a[1]);
-        row[1].upd = 1;
-        for (int k = 2; k <= dj; ++k) {
-          const int r = (k - 1) % 3;  // regular update every third term covers k-2..k
-          const int nterm = (r == 0) ? 3 : (k == dj ? r : 0);
-          row[k].upd = nterm > 0;
-          if (nterm >= 3) put(row[k].c[0], a[k - 2]);
-          if (nterm >= 2) put(row[k].c[1], a[k - 1]);
-          if (nterm >= 1) put(row[k].c[2], a[k]);
-        }
       }
-    const size_t cb = coef.size() * sizeof(CoefK);
-    if (cb > P.coef_bytes) {
-      if (P.coef) (void)hipFree(P.coef), P.coef = nullptr;
-      if (hipMalloc(&P.coef, cb) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "coefficient allocation failed");
-      P.coef_bytes = cb;
-    }
-    HIPC(hipMemcpy(P.coef, coef.data(), cb, hipMemcpyHostToDevice));
     DevProb& d = ctx->h_desc[pi];
-    d.coef = P.coef;
     d.kcap1 = kcap1;
     d.degree = deg;
     d.beta = beta;
     d.s1 = 1.0 / alpha;
     d.n_acc = M;
+  };
+  if (ctx->dbg & 4)
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi) coef_one(pi);
+  else
+    parallel_for(ctx->probs.size(), coef_one);
+  Arena coef_arena;
+  std::vector<size_t> coef_off(ctx->probs.size(), 0);
+  size_t coef_total = 0;
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    if (coef_rc[pi] != DSE_OK) return fail(ctx, coef_rc[pi], coef_msg[pi]);
+    coef_total += align_up(coef_rows[pi].size() * sizeof(double2), 64);
+  }
+  coef_arena.host.reserve(coef_total);
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+    if (!ctx->probs[pi].sm) coef_off[pi] = coef_arena.place(coef_rows[pi].size() * sizeof(double2));
+  parallel_for(ctx->probs.size(), [&](size_t pi) {
+    if (!coef_rows[pi].empty())
+      std::memcpy(coef_arena.host.data() + coef_off[pi], coef_rows[pi].data(), coef_rows[pi].size() * sizeof(double2));
+  });
+
+  phase("coefficients");
+  if ((rc = upload_arena(ctx, coef_arena, &ctx->d_coef, &ctx->coef_cap, ctx->lanes[0].stream))) return rc;
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+    HostProblem& P = ctx->probs[pi];
+    if (P.sm) continue;
+    P.coef = reinterpret_cast<double2*>(ctx->d_coef + coef_off[pi]);
+    ctx->h_desc[pi].coef = P.coef;
   }
 
+  phase("coef upload");
   // intermediate outputs of multi-output launches: (M - 1) state vectors per problem
   {
     size_t need = 0;
@@ -1766,23 +1860,48 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   }
   int* d_err = persistent ? ctx->d_flags + 2 * ctx->probs.size() : nullptr;
 
+  phase("lanes/items");
   // ---- psi(t0) = |psi0> ----
   hipStream_t st0 = ctx->lanes[0].stream;
-  for (auto& P : ctx->probs) {
-    const size_t vbytes = (size_t(1) << P.n_local) * sizeof(double2);
-    HIPC(hipMemsetAsync(P.buf[0], 0, vbytes, st0));
-    static const double2 one = {1.0, 0.0};
-    if ((P.psi0 >> P.n_local) == (uint64_t)P.shard_rank) {  // the shard holding psi0
-      const uint64_t local = P.psi0 & ((uint64_t(1) << P.n_local) - 1);
-      HIPC(hipMemcpyAsync(P.buf[0] + local, &one, sizeof(double2), hipMemcpyHostToDevice, st0));
+  {
+    std::vector<BasisInit> init;
+    uint64_t max_amps = 0;
+    for (auto& P : ctx->probs) {
+      BasisInit e;
+      e.ptr = P.buf[0];
+      e.n = uint64_t(1) << P.n_local;
+      // the shard holding psi0 (every unsharded register)
+      e.one_at = ((P.psi0 >> P.n_local) == (uint64_t)P.shard_rank)
+                     ? (int64_t)(P.psi0 & ((uint64_t(1) << P.n_local) - 1)) : -1;
+      init.push_back(e);
+      max_amps = std::max(max_amps, e.n);
     }
+    if (init.size() > ctx->init_cap) {
+      if (ctx->d_init) (void)hipFree(ctx->d_init), ctx->d_init = nullptr;
+      ctx->init_cap = 0;
+      if (hipMalloc(&ctx->d_init, init.size() * sizeof(BasisInit)) != hipSuccess)
+        return fail(ctx, DSE_ERR_OOM, "initial-state list allocation failed");
+      ctx->init_cap = init.size();
+    }
+    if (ctx->dbg & 2) {
+      for (auto& e : init) {
+        HIPC(hipMemsetAsync(e.ptr, 0, e.n * sizeof(double2), st0));
+        static const double2 one = {1.0, 0.0};
+        if (e.one_at >= 0) HIPC(hipMemcpyAsync(e.ptr + e.one_at, &one, sizeof(double2), hipMemcpyHostToDevice, st0));
+      }
+    } else {
+      HIPC(hipMemcpyAsync(ctx->d_init, init.data(), init.size() * sizeof(BasisInit), hipMemcpyHostToDevice, st0));
+      for (size_t i0 = 0; i0 < init.size(); i0 += 65535)
+        HIPC(launch_basis_init(ctx->d_init + i0, (int)std::min<size_t>(65535, init.size() - i0), max_amps, st0));
+    }
+    HIPC(hipStreamSynchronize(st0));
   }
-  HIPC(hipStreamSynchronize(st0));
   double small_happl = 0.0, small_launches = 0.0;
   if (any_small && (rc = small_launch(ctx, t, n_t, tol, &small_happl, &small_launches))) return rc;
 
-  const size_t chunk = (size_t)std::min<int64_t>(
-      n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64)));
+  phase("psi0/small");
+  const size_t chunk = (size_t)std::max<int64_t>(M, std::min<int64_t>(
+      n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64))));
   if ((rc = ensure_partial(ctx, chunk))) return rc;
   if (ctx->time_every > 0)
     for (auto& ln : ctx->lanes) {
@@ -1818,20 +1937,21 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     pool_amps[li * 2 + pool].clear();
     return DSE_OK;
   };
-  auto obs_all = [&](int bsel_q, size_t slot) -> int {
+  // observables of n_out consecutive output slots (one launch per lane group): outputs
+  // j < n_out - 1 from the intermediate accumulators, the last from state role bsel_q
+  auto obs_all = [&](int bsel_q, size_t slot, int n_out) -> int {
     for (auto& ln : ctx->lanes)
-      for (auto& g : ln.groups) {
-        const int bsel = bsel_q;
-        HIPC(launch_obs(g.L, ctx->d_probs, ctx->d_items + g.off, (int)g.count, bsel,
-                        ctx->d_partial + (slot * ctx->total_items + g.off) * 8, ln.stream));
-      }
+      for (auto& g : ln.groups)
+        HIPC(launch_obs(g.L, ctx->d_probs, ctx->d_items + g.off, (int)g.count, bsel_q,
+                        ctx->d_partial + (slot * ctx->total_items + g.off) * 8, ln.stream, n_out,
+                        (size_t)ctx->total_items * 8));
     return DSE_OK;
   };
 
   std::vector<double> dist_raw(any_dist ? ctx->probs.size() * (size_t)n_t * 7 : 0, 0.0);
   size_t slot = 0, t_flushed = 0;
   if (any_dist && (rc = dist_exchange(ctx, 0, 0, ctx->lanes[0].stream))) return rc;
-  if ((rc = obs_all(0, slot++))) return rc;
+  if ((rc = obs_all(0, slot++, 1))) return rc;
   for (int gi = 0; gi < n_groups; ++gi) {
     const Group& G = groups[gi];
     const int q = gi & 1;
@@ -1910,15 +2030,30 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     // new psi of every problem sits in acc(q) = buf[q ? 0 : 2]; outputs j < n_out - 1 of a
     // multi-output launch in the intermediate accumulators
     if (any_dist && (rc = dist_exchange(ctx, q ? 0 : 2, 0, ctx->lanes[0].stream))) return rc;
-    for (int j = 0; j < G.n_out; ++j) {
-      if ((rc = obs_all(j == G.n_out - 1 ? (q ? 0 : 2) : 3 + j, slot++))) return rc;
-      if (slot == chunk) {
-        if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
-        t_flushed += slot;
-        slot = 0;
+    if (slot + G.n_out > chunk) {  // the group's outputs share one launch: one chunk
+      if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
+      t_flushed += slot;
+      slot = 0;
+    }
+    if (ctx->dbg & 1) {
+      for (int j = 0; j < G.n_out; ++j) {
+        for (auto& ln : ctx->lanes)
+          for (auto& g : ln.groups)
+            HIPC(launch_obs(g.L, ctx->d_probs, ctx->d_items + g.off, (int)g.count,
+                            j == G.n_out - 1 ? (q ? 0 : 2) : 3 + j,
+                            ctx->d_partial + ((slot + j) * ctx->total_items + g.off) * 8, ln.stream));
       }
+    } else if ((rc = obs_all(q ? 0 : 2, slot, G.n_out))) {
+      return rc;
+    }
+    slot += G.n_out;
+    if (slot == chunk) {
+      if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
+      t_flushed += slot;
+      slot = 0;
     }
   }
+  phase("launch loop");
   if (slot > 0) {
     if ((rc = flush_partials(ctx, slot, t_flushed, n_t, obs_out, &dist_raw))) return rc;
     t_flushed += slot;
@@ -1928,6 +2063,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       if ((rc = drain(ctx->lanes[li], li, pool))) return rc;
   if ((rc = sync_all(ctx))) return rc;
   if ((rc = small_gather(ctx, n_t, obs_out))) return rc;
+  phase("flush/drain");
   if (persistent && any_big) {
     int herr = 0;
     HIPC(hipMemcpy(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -1956,6 +2092,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
                    obs_out + pi * DSE_N_OBS * (size_t)n_t + ti, (size_t)n_t);
     }
   }
+  phase("tail");
   ctx->last_q = n_groups & 1;
   for (auto& P : ctx->probs) P.final_bsel = P.sm ? 0 : (ctx->last_q ? 2 : 0);
   ctx->evolved = true;

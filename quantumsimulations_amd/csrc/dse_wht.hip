@@ -402,7 +402,7 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     gd2* acc_b = gptr(P.buf[q ? 0 : 2]);
     gd2* scr_b = gptr(P.buf[1]);
     CoefK C = {};
-    if (MODE != MODE_APPLY) C = P.coef[set * P.kcap1 + (MODE == MODE_FIRST ? 1 : k)];
+    if (MODE != MODE_APPLY) C = coef_at(coef_row(P, set, 0), MODE == MODE_FIRST ? 1 : k);
     gd2* wdst = (MODE == MODE_GEN && !(k & 1)) ? psi_b : scr_b;  // GEN: holds w_{k-2}
     const double scale = MODE == MODE_GEN ? 2.0 * P.s1 : P.s1;
 #pragma unroll

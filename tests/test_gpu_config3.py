@@ -84,3 +84,23 @@ def test_production_interval_kernel_matches_reference_n14(engine, golden, m):
             assert err < 1e-10, (key, k, err)
         np.testing.assert_allclose(obs[i, 6], g[f"{key}_state_norm"], rtol=0, atol=1e-12)
     print(f"N=14 production path (M={m}): max |GPU - reference-H oracle| = {worst:.2e}")
+
+
+@pytest.mark.parametrize("m", [2, 1])
+def test_production_path_is_repeatable_in_one_context(engine, m):
+    """The same evolve of the config-3 points, three times in one context (same allocations, same
+    hand-off slots and flags): bitwise identical.  A build whose interval kernel read its
+    coefficient rows through scalar loads varied here at the 1e-10 level (tools/diag_repeat.py)."""
+    t = np.linspace(0.0, 2e-4, 21)
+    engine.clear()
+    engine.set_option("outputs_per_launch", m)
+    try:
+        for variant in VARIANTS:
+            for delta in DELTAS:
+                engine.add(pb.build_problem(_params(variant, delta, t)))
+        runs = [engine.evolve(t)[0] for _ in range(3)]
+    finally:
+        engine.set_option("outputs_per_launch", 2)
+        engine.clear()
+    for r in runs[1:]:
+        assert np.array_equal(r, runs[0])
