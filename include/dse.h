@@ -133,7 +133,11 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         (default: tile bits - 2)
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
- *          "max_degree"   Chebyshev degree cap per interval (default 2e6) */
+ *          "max_degree"   Chebyshev degree cap per interval (default 2e6)
+ *          "handoff_fences"  persistent mode, 2-tile registers: 0 (default) the sc1 hand-off
+ *                         (write-through payload, per-wave vmcnt(0) + barrier, sc1 flag and
+ *                         poll); 1 adds an agent-scope release before every flag store and an
+ *                         acquire after every poll */
 int dse_set_option(dse_ctx* ctx, const char* key, double value);
 
 /* ---- problems ----------------------------------------------------------------------------- */

@@ -144,6 +144,7 @@ hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items,
 hipError_t set_ablate(int mask);
 hipError_t set_ablate_interval(int mask);
 hipError_t set_spin_limit(int limit);
+hipError_t set_handoff_fences(int on);  // interval kernel: release/acquire around each hand-off
 bool interval_supported(int L);
 // resident workgroups of k_interval<L> per compute unit (occupancy query)
 hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu);

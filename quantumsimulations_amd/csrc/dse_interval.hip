@@ -47,6 +47,12 @@ __device__ int g_dse_ablate_iv = 0;
 // ~0.3 s at the default).  Diagnostics: a negative value fails every hand-off at its first wait,
 // which exercises the runtime's fallback to the streaming kernels.
 __device__ int g_dse_spin_limit = 1 << 22;
+// Hand-off protocol: 0 (default) the sc1 form -- sc1 payload stores and loads, per-wave
+// s_waitcnt vmcnt(0) + barrier before an sc1 flag store, sc1 poll (MI355X_MICROARCH.md, Valid
+// forms, table row 1); 1 adds an agent-scope release in front of every flag store and an
+// agent-scope acquire behind every poll (the placement-independent Guideline 16 recipe): -2.8%
+// points/h on the bench (profiles/r02/ab/handoff_fences.jsonl).
+__device__ int g_dse_handoff_fences = 0;
 
 hipError_t set_ablate_interval(int mask) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_ablate_iv), &mask, sizeof(int));
@@ -54,6 +60,10 @@ hipError_t set_ablate_interval(int mask) {
 
 hipError_t set_spin_limit(int limit) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_spin_limit), &limit, sizeof(int));
+}
+
+hipError_t set_handoff_fences(int on) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_handoff_fences), &on, sizeof(int));
 }
 
 namespace {
@@ -166,6 +176,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   // the register-bit terms, 64 skip the hand-off stores and flag, 128 skip the partner wait and
   // read, 256 skip the acc updates, 512 skip the tile terms
   const int ab = g_dse_ablate_iv;
+  const bool fences = g_dse_handoff_fences != 0;
 
   // ---- setup: tables, w_0 tile -> LDS, per-thread diagonal ----
   if (tid == 0) s_fail = 0;
@@ -322,7 +333,13 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       if (pair && !(ab & 64) && (xgen || k > 1)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+          if (fences) {  // agent-scope release in front of the flag (Guideline 16 form)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     };
     if (kPublishAfter == 1) publish();
@@ -411,6 +428,10 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
               atomicExch(err, 1);
               break;
             }
+          }
+          if (fences) {  // agent-scope acquire behind the poll
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
         }
         __syncthreads();

@@ -1000,6 +1000,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "small_chunk") {
     if (!(value >= 1 && value <= 1e6)) return fail(ctx, DSE_ERR_ARG, "small_chunk must be in 1..1e6");
     ctx->small_chunk = (int)value;
+  } else if (k == "handoff_fences") {  // interval kernel: agent release/acquire around each hand-off
+    HIPC(set_handoff_fences(value != 0.0));
   } else if (k == "spin_limit") {  // diagnostics: partner-flag polls per hand-off (< 0: always fail)
     HIPC(set_spin_limit((int)value));
   } else if (k == "xcd_pairs") {

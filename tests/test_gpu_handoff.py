@@ -81,3 +81,26 @@ def test_two_tile_launch_beside_a_busy_device(engine):
     for obs, st in runs:
         assert st["mode"] in (0, 1)
         np.testing.assert_allclose(obs, alone, rtol=0, atol=1e-12)
+
+
+def test_handoff_with_release_acquire_fences(engine):
+    """Option handoff_fences = 1 (agent-scope release before each flag store, acquire after each
+    poll): the same results as the default sc1 hand-off, bitwise repeatable."""
+    t = np.linspace(0.0, 1e-4, 11)
+    probs = [pb.build_problem(sweep_point_params(13, 60e3, v, 1e-4, 11)) for v in ("center_on", "shell_off")]
+    res = {}
+    for f in (0, 1, 1):
+        engine.clear()
+        engine.set_option("handoff_fences", f)
+        try:
+            for p in probs:
+                engine.add(p)
+            obs, st = engine.evolve(t)
+        finally:
+            engine.set_option("handoff_fences", 0)
+        assert st["mode"] == 1
+        if f in res:
+            assert np.array_equal(obs, res[f])
+        res[f] = obs
+    np.testing.assert_allclose(res[1], res[0], rtol=0, atol=1e-13)
+    engine.clear()
