@@ -20,6 +20,7 @@ __host__ __device__ constexpr int rr_index(int a, int b) {
   return a * (2 * kRegBits - a - 1) / 2 + (b - a - 1);
 }
 constexpr int kXSlots = 4;                        // hand-off ring of the interval kernel
+constexpr int kIvWaves = 8;                       // hand-off flags per tile (one per wave of a 2^13 tile)
 #ifndef DSE_MAX_OUT
 #define DSE_MAX_OUT 2
 #endif

@@ -27,12 +27,15 @@
 //     B applies the flip coefficient itself, so A hands over w_{k-1} raw.  A stores w_k with
 //     16-byte sc1 stores at the end of term k (w_0 is A's psi tile, readable as is);
 //   * crossing pairs (shell geometry): A computes u in a pre-pass at the start of the term.
-// Either way the stores drain under phase 1, then the tile publishes the term index with an sc1
-// flag store (after s_waitcnt vmcnt(0) and a barrier); the partner polls the flag with sc1 loads
-// (one lane, s_sleep, bounded), barriers and reads the operand with sc1 loads after phase 3
-// (MI355X_MICROARCH.md "Valid forms", row 1: one workgroup per CU).  Slots form a ring of
-// kXSlots per tile; a slot is rewritten kXSlots terms later, and every term waits for the
-// partner's flag of that term, so the partner has long finished reading it.
+// Thread t of one tile reads only the rows of thread t of the other, so the hand-off is per wave:
+// after its first tile phase each wave waits for its own stores (s_waitcnt vmcnt(0)) and one lane
+// publishes the term index with an sc1 flag store for that wave; the partner's wave of the same
+// index polls it with sc1 loads (one lane, s_sleep, bounded) and reads the operand with sc1 loads
+// after its tile phases (MI355X_MICROARCH.md "Valid forms", row 1, per wave: one workgroup per CU).
+// No workgroup barrier is involved, which lets waves 4..7 run the tile phases in the opposite order
+// to their SIMD partners 0..3.  Slots form a ring of kXSlots per tile; a slot is rewritten kXSlots
+// terms later, and every term waits for the partner wave's flag of that term, so the partner wave
+// has long finished reading it.
 //
 // Register budget: this kernel must not spill VGPRs.  A build that spilled 12 VGPRs (stored once in
 // the prologue, reloaded every term) gave run-to-run differences of ~1e-9 on 2-tile problems;
@@ -68,14 +71,6 @@ hipError_t set_handoff_fences(int on) {
 
 namespace {
 
-#ifndef DSE_PUBLISH_AFTER
-#define DSE_PUBLISH_AFTER 2
-#endif
-// Hand-off flag of term k published after phase 1 or after phase 2 (the sweeps): later gives the
-// write-through stores more time to drain before the per-wave vmcnt(0) wait, earlier gives the
-// partner more slack before it needs the flag (its phase 4).
-constexpr int kPublishAfter = DSE_PUBLISH_AFTER;
-
 typedef __attribute__((address_space(1))) int gint;
 
 
@@ -105,24 +100,15 @@ struct IvShared {
   // registers: the kernel is at the 256-VGPR limit and these are read once per term
   double td[1 + kRegBits][RB<L>::NT];
   double xg[kRegBits];  // cross pairs (register bit i, top bit) of the u pre-pass
+  DSweep sw[RB<L>::TB];        // thread-bit sweeps (LDS copies of P.sweeps: counted waits, no SMEM)
+  DPair tt[4 * RB<L>::TB];     // thread-bit pairs, zero-padded to four per sweep
 };
-
-// Sweep pairs (thread bit j, register bit i < 3) of half hh for a wave-uniform bit value BJ.
-template <int BJ, int NH>
-__device__ __forceinline__ void sweep_pairs_uniform(const double* g, const double2* pv, double2* out_h) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int rr = 0; rr < NH; ++rr)
-      if (((rr >> i) & 1) == BJ) rmad(out_h[rr], g[i], pv[rr ^ (1 << i)]);
-}
 
 template <int L, bool IMAG>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
            int n_out, int* __restrict__ flags, int* __restrict__ err) {
   constexpr int NT = RB<L>::NT, R = kRegAmps, TB = RB<L>::TB, NH = R / 2;
-  constexpr int LANE_BITS = TB < 6 ? TB : 6;
   constexpr uint32_t T = 1u << L;
   __shared__ IvShared<L> S;
   __shared__ int s_fail;
@@ -148,12 +134,13 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   double2* const xs_pa = P.xslots + ((size_t)(h ^ 1u) * kXSlots << L);
   const __amdgpu_buffer_rsrc_t acc_t = tile_rsrc(P.buf[q ? 0 : 2] + (h << L), TBYTES);
   const uint32_t voff = (uint32_t)tid * 16u;
-  gint* flag_me = (gint*)flags + 2 * it.x + h;
-  const gint* flag_pa = (const gint*)flags + 2 * it.x + (h ^ 1u);
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // hand-off flags: one per wave, flags[(2 * problem + tile) * kIvWaves + wave]
+  gint* flag_me = (gint*)flags + (2 * it.x + (int)h) * kIvWaves + wave;
+  const gint* flag_pa = (const gint*)flags + (2 * it.x + (int)(h ^ 1u)) * kIvWaves + wave;
 
   // term tables (scalar loads)
-  const cptr<DSweep> csw = cst(P.sweeps);
-  const cptr<DPair> ctt = cst(P.pairs_tt);
   const cptr<DPair> cph = cst(P.pairs_hi);
   const cptr<DFlip> cfh = cst(P.flips_hi);
   // coefficient rows of the outputs (coef_row): [j][0].x = degree d_j, [j][1 + k] = a_k
@@ -164,13 +151,6 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   int dj[kMaxOut];
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) dj[j] = j < n_out ? (int)crow[j * rstride] : 0;
-  const int n_tt = P.n_pairs_tt;
-  // the top-bit drive (cross flip) for this tile's output bit value (raw exchange)
-  double xr = 0.0, xi = 0.0;
-  if (pair && P.n_flips_hi > 0) {
-    xr = b_me ? cfh[0].re1 : cfh[0].re0;
-    xi = b_me ? cfh[0].im1 : cfh[0].im0;
-  }
 
   // diagnostics only (0 in production): 1 skip the sweeps, 2 skip the thread-bit pairs, 4 skip
   // the register-bit terms, 64 skip the hand-off stores and flag, 128 skip the partner wait and
@@ -188,6 +168,14 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       S.zz[e] = (j > i) ? zz[i * n + j] : 0.0;
     }
     tile_diag_coeffs<L>(P, h, P.beta, S.c, tid);
+    stage16(S.sw, P.sweeps, TB * (int)(sizeof(DSweep) / 16), tid, NT);
+    const gd2* ptt = (const gd2*)P.pairs_tt;
+    for (int e = tid; e < 4 * TB; e += NT) {  // DPair is one 16-byte granule; zero past the list
+      dv2 v;
+      v.x = v.y = 0.0;
+      if (e < P.n_pairs_tt) v = ptt[e];
+      reinterpret_cast<dv2*>(S.tt)[e] = v;
+    }
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) S.w[r * NT + tid] = bld(psi_me, voff, (uint32_t)(r * NT * 16));
@@ -327,13 +315,14 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       }
     }
 
-    // ---- publish: every wave's hand-off stores of this term have drained (s_waitcnt vmcnt(0)
-    // per wave, then the barrier), then one lane stores the term index as the flag (sc1) ----
+    // ---- publish (per wave): thread t's hand-off rows are read only by thread t of the partner
+    // tile, i.e. wave w's stores only by the partner's wave w.  The wave waits for its own stores
+    // (s_waitcnt vmcnt(0)) and one lane stores the term index to the wave's flag (sc1); no
+    // workgroup barrier, so the two halves of the workgroup can run their phases in either order ----
     auto publish = [&]() {
       if (pair && !(ab & 64) && (xgen || k > 1)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
+        if (lane == 0) {
           if (fences) {  // agent-scope release in front of the flag (Guideline 16 form)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -342,83 +331,76 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         }
       }
     };
-    if (kPublishAfter == 1) publish();
 
-    if (!(ab & 512)) {
-      // ---- phase 2: thread-bit sweeps ----
+    // ---- phases 2 + 3, fused: iteration j = the LDS sweep of thread bit j (its drive and its pairs
+    // with the register bits; VALU-heavy) + thread-bit pairs 4j .. 4j + 3 (partner t ^ e_i ^ e_j,
+    // coefficient zero in the lanes with x_i != x_j; LDS-heavy), one basic block, so the pairs'
+    // partner reads issue under the sweep's FMAs.  The hand-off is published half way. ----
+    // ---- phase 4 (after the fused loop below): the partner tile's contribution, read with sc1 loads
+    // after one poll of the partner wave's flag ----
+    constexpr int J_PUB = TB / 2;  // publish half way through the fused loop
+
 #pragma unroll 1
-      for (int j = 0; j < ((ab & 1) ? 0 : TB); ++j) {
-        const int has_flip = csw[j].has_flip, has_pair = csw[j].has_pair;
-        if (!(has_flip | has_pair)) continue;
-        const int bj = (tid >> j) & 1;
-        const int pt = tid ^ (1 << j);
-        const double cr = bj ? csw[j].re1 : csw[j].re0, ci = bj ? csw[j].im1 : csw[j].im0;
-        double g[kRegBits];
+    for (int j = 0; j < ((ab & 512) ? 0 : TB); ++j) {
+      if (j == J_PUB) publish();
+      const DSweep sw = S.sw[j];
+      const int bj = (tid >> j) & 1;
+      const int pt = tid ^ (1 << j);
+      const double sk = (ab & 1) ? 0.0 : 1.0;
+      const double cr = sk * (bj ? sw.re1 : sw.re0), ci = sk * (bj ? sw.im1 : sw.im0);
+      double g0[kRegBits], g1[kRegBits];  // pair (j, register bit i) on rows with r_i = 0 / 1
 #pragma unroll
-        for (int i = 0; i < kRegBits; ++i) g[i] = csw[j].g[i];
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          double2 pv[NH];
-#pragma unroll
-          for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
-          double2* oh = out + hh * NH;
-          if (has_flip) {
-#pragma unroll
-            for (int rr = 0; rr < NH; ++rr) oh[rr] = dmad<IMAG>(oh[rr], cr, ci, pv[rr]);
-          }
-          if (has_pair) {
-            if (j >= LANE_BITS) {  // a wave-index bit: bj is uniform, touch only the rows it pairs
-              if (bj)
-                sweep_pairs_uniform<1, NH>(g, pv, oh);
-              else
-                sweep_pairs_uniform<0, NH>(g, pv, oh);
-            } else {
-#pragma unroll
-              for (int i = 0; i < 3; ++i) {
-                const double g0 = bj ? 0.0 : g[i], g1 = bj ? g[i] : 0.0;  // iff r_i == bj
-#pragma unroll
-                for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ((rr >> i) & 1) ? g1 : g0, pv[rr ^ (1 << i)]);
-              }
-            }
-            // (j, register bit 3): rows of the other half, iff r_3 = 1 - hh == bj
-            const double g3 = (1 - hh == bj) ? g[3] : 0.0;
-            double2* oo = out + (1 - hh) * NH;
-#pragma unroll
-            for (int rr = 0; rr < NH; ++rr) rmad(oo[rr], g3, pv[rr]);
-          }
-        }
+      for (int i = 0; i < kRegBits; ++i) {
+        g0[i] = bj ? 0.0 : sk * sw.g[i];
+        g1[i] = bj ? sk * sw.g[i] : 0.0;
       }
-
-      if (kPublishAfter == 2) publish();  // the stores drained under phases 1 and 2
-
-      // ---- phase 3: pairs between two thread bits ----
-#pragma unroll 1
-      for (int p = 0; p < ((ab & 2) ? 0 : n_tt); ++p) {
-        const uint32_t m = ctt[p].mask_lo;
-        if (par32((uint32_t)tid & m)) continue;  // rows with x_i == x_j
-        const double g = ctt[p].g;
-        const int pt = tid ^ (int)m;
+      int tpt[4];
+      double ge[4];
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          double2 pv[NH];
+      for (int qq = 0; qq < 4; ++qq) {
+        const DPair e = S.tt[4 * j + qq];  // zero entries beyond the problem's pairs
+        tpt[qq] = tid ^ (int)e.mask_lo;
+        ge[qq] = (par32((uint32_t)tid & e.mask_lo) || (ab & 2)) ? 0.0 : e.g;  // rows with x_i == x_j
+      }
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+      for (int hh = 0; hh < 2; ++hh) {
+        double2 pv[NH];
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) rmad(out[hh * NH + rr], g, pv[rr]);
+        for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+        double2* oh = out + hh * NH;
+#pragma unroll
+        for (int rr = 0; rr < NH; ++rr) oh[rr] = dmad<IMAG>(oh[rr], cr, ci, pv[rr]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ((rr >> i) & 1) ? g1[i] : g0[i], pv[rr ^ (1 << i)]);
+        // (j, register bit 3): rows of the other half, r_3 = 1 - hh
+        double2* oo = out + (1 - hh) * NH;
+        const double g3 = hh ? g0[3] : g1[3];
+#pragma unroll
+        for (int rr = 0; rr < NH; ++rr) rmad(oo[rr], g3, pv[rr]);
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          double2 tv[NH];
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) tv[rr] = S.w[(hh * NH + rr) * NT + tpt[qq]];
+#pragma unroll
+          for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ge[qq], tv[rr]);
         }
       }
     }
-
-    if (kPublishAfter == 2 && (ab & 512)) publish();
-
-    // ---- phase 4: the partner tile's contribution ----
+    if (ab & 512) publish();  // diagnostics: no tile terms, the hand-off alone
     if (pair && !(ab & 128)) {
-      // operand of term k: slot k of the partner, or (raw exchange, k = 1) its psi tile
-      const __amdgpu_buffer_rsrc_t src =
+      const __amdgpu_buffer_rsrc_t src =  // operand of term k: partner slot, or (raw, k = 1) its psi
           (xraw && k == 1) ? psi_pa : tile_rsrc(xs_pa + ((size_t)((k - 1) % kXSlots) << L), TBYTES);
-      const bool need_flag = xgen || k > 1;  // w_0 of the partner is its psi tile, already visible
-      if (need_flag) {
-        if (tid == 0 && !(ab & 64)) {
+      // the top-bit drive (cross flip) at this tile's output bit value (raw exchange; scalar loads
+      // here rather than registers held across the term)
+      double xr = 0.0, xi = 0.0;
+      if (xraw && P.n_flips_hi > 0) {
+        xr = b_me ? cfh[0].re1 : cfh[0].re0;
+        xi = b_me ? cfh[0].im1 : cfh[0].im0;
+      }
+        if ((xgen || k > 1) && lane == 0 && !(ab & 64)) {  // w_0 of the partner is its psi tile
           int spins = 0;
           const int limit = g_dse_spin_limit;
           while (limit < 0 || __hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
@@ -434,22 +416,20 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
         }
-        __syncthreads();
-      }
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         double2 uv[NH];
 #pragma unroll
         for (int rr = 0; rr < NH; ++rr) uv[rr] = bld<kSc1>(src, voff, (uint32_t)((hh * NH + rr) * NT * 16));
-        if (xgen) {
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) {
-            out[hh * NH + rr].x += uv[rr].x;
-            out[hh * NH + rr].y += uv[rr].y;
+        for (int rr = 0; rr < NH; ++rr) {
+          double2& o = out[hh * NH + rr];
+          if (xgen) {
+            o.x += uv[rr].x;
+            o.y += uv[rr].y;
+          } else {
+            o = dmad<IMAG>(o, xr, xi, uv[rr]);
           }
-        } else {
-#pragma unroll
-          for (int rr = 0; rr < NH; ++rr) out[hh * NH + rr] = dmad<IMAG>(out[hh * NH + rr], xr, xi, uv[rr]);
         }
       }
     }
@@ -526,14 +506,17 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 // launches of another stream, whose problems' flags are in use, are not disturbed
 __global__ void k_zero_flags(const int2* __restrict__ items, int n_items, int* __restrict__ flags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_items) flags[2 * items[i].x + items[i].y] = 0;
+  if (i < n_items * kIvWaves) {
+    const int2 e = items[i / kIvWaves];
+    flags[(2 * e.x + e.y) * kIvWaves + i % kIvWaves] = 0;
+  }
 }
 
 }  // namespace
 
 hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_zero_flags, dim3((n_items + 255) / 256), dim3(256), 0, st, items, n_items, flags);
+  hipLaunchKernelGGL(k_zero_flags, dim3((n_items * kIvWaves + 255) / 256), dim3(256), 0, st, items, n_items, flags);
   return hipGetLastError();
 }
 

@@ -126,7 +126,7 @@ struct dse_ctx {
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
   int handoff_fallbacks = 0;        // evolves re-run on the streaming kernels after a hand-off timeout
-  int* d_flags = nullptr;           // hand-off flags (2 per problem) + error word
+  int* d_flags = nullptr;           // hand-off flags (2 tiles x kIvWaves per problem) + error word
   size_t flags_cap = 0;
   double2* d_xslots = nullptr;      // hand-off slots of the interval kernel
   size_t xslot_cap = 0;             // in amplitudes
@@ -1851,7 +1851,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     HIPC(hipMemcpy(ctx->d_items_iv, iv.data(), iv.size() * sizeof(int2), hipMemcpyHostToDevice));
   }
   if (persistent) {
-    const size_t need = 2 * ctx->probs.size() + 1;  // flags, error word
+    const size_t need = 2 * kIvWaves * ctx->probs.size() + 1;  // flags, error word
     if (ctx->flags_cap < need) {
       if (ctx->d_flags) (void)hipFree(ctx->d_flags), ctx->d_flags = nullptr;
       if (hipMalloc(&ctx->d_flags, need * sizeof(int)) != hipSuccess)
@@ -1860,7 +1860,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     }
     HIPC(hipMemset(ctx->d_flags, 0, need * sizeof(int)));
   }
-  int* d_err = persistent ? ctx->d_flags + 2 * ctx->probs.size() : nullptr;
+  int* d_err = persistent ? ctx->d_flags + 2 * kIvWaves * ctx->probs.size() : nullptr;
 
   phase("lanes/items");
   // ---- psi(t0) = |psi0> ----
