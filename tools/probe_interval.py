@@ -21,10 +21,19 @@ from quantumsimulations_amd.engine import Engine  # noqa: E402
 from quantumsimulations_amd.sweep import sweep_params  # noqa: E402
 
 
+def keep(p, which):
+    if which == "all":
+        return True
+    if which in ("pairs", "singles"):
+        return (which == "pairs") == (p.n_qubits == 14)
+    # "center_on" / "shell_off": the 2-tile problems of one variant (raw / generated hand-off)
+    return p.n_qubits == 14 and p.meta.get("_v") == which
+
+
 def run(eng, probs, t, mask, which):
     eng.clear()
     for p in probs:
-        if which == "all" or (which == "pairs") == (p.n_qubits == 14):
+        if keep(p, which):
             eng.add(p)
     eng.set_option("ablate", 0)
     eng.evolve(t)
@@ -40,16 +49,22 @@ def run(eng, probs, t, mask, which):
 
 def main():
     params = sweep_params(13, np.linspace(0.0, 150e3, 64), 1e-3, 101)
-    probs = [pb.build_problem(p) for p in params]
+    probs = []
+    for p in params:
+        pr = pb.build_problem(p)
+        pr.meta["_v"] = "center_on" if (p.is_center_rare and pr.rare_bit >= 0) else (
+            "center_off" if p.is_center_rare else "shell_off")
+        probs.append(pr)
+    sets = sys.argv[1].split(",") if len(sys.argv) > 1 else ["pairs", "singles", "all"]
     t = np.linspace(0.0, 1e-5, 2)
     eng = Engine(0, tile_bits=13)
     eng.set_option("streams", 1)
-    for which in ("pairs", "singles", "all"):
+    for which in sets:
         for name, mask in (("full", 0), ("no_publish", 64), ("no_wait_read", 128),
                            ("no_exchange", 64 | 128), ("no_acc", 256), ("no_tile_terms", 512),
                            ("exchange_only", 256 | 512), ("no_sweeps", 1), ("no_tt_pairs", 2),
                            ("no_register_terms", 4), ("register_terms_only", 1 | 2)):
-            if which != "pairs" and mask & (64 | 128):
+            if which in ("singles", "all") and mask & (64 | 128):
                 continue
             ms, st = run(eng, probs, t, mask, which)
             print(json.dumps({"set": which, "config": name, "ablate": mask, "ms_per_launch": ms,
