@@ -26,12 +26,18 @@ Extra fields of the JSON line:
                  the host cores, 1 core and all cores, run before the GPU is touched
   large_register rank 0, N = 1 only: config 5 on one GPU (N = 30, Walsh-Hadamard engine) against
                  the HBM roofline, with exact-invariant checks (norm, energy); --no-large skips it
+  partitioned    N = 2, 4, 8 only, after the timed sweep: config 5 with the N = 30 register split
+                 over the N ranks (tools/bench_partitioned.py as a child process per rank, RCCL
+                 index-swap all-to-all over xGMI): ms per H application, exchanged bytes per rank,
+                 norm check; bounded by a timeout, reported (never raised) on failure
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -68,6 +74,8 @@ def parse():
     ap.add_argument("--no-full", action="store_true", help="skip the reference-grid (30 s) leg")
     ap.add_argument("--full-intervals", type=int, default=2,
                     help="output intervals of the 30 s reference grid timed by the full-sweep leg")
+    ap.add_argument("--partitioned-timeout", type=float, default=180.0,
+                    help="N > 1: seconds allowed for the config-5 partitioned leg (child processes)")
     ap.add_argument("--cpu-cores", type=int, default=int(os.environ.get("DSE_CPU_CORES", "0")),
                     help="worker processes of the all-core CPU leg (0: this process's CPU share)")
     return ap.parse_args()
@@ -244,6 +252,55 @@ def timed_steps(step, steps: int, warmup: int, sync, dist=None) -> float:
     return dt
 
 
+def note(msg: str) -> None:
+    """Progress on stderr (the JSON line is the only stdout)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def partitioned_leg(rank: int, world: int, local: int, dist, timeout: float, cmd=None) -> dict:
+    """Config 5 across the job's ranks: every rank starts tools/bench_partitioned.py as a child
+    process (its own gloo bootstrap on a fresh port, libdse's RCCL communicator for the data path)
+    and waits for it with a timeout; rank 0's child prints the JSON line.  A failure or a hang
+    ends in a report, never in an exception or a hung bench."""
+    box = [None]
+    if rank == 0:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        box[0] = s.getsockname()[1]
+        s.close()
+    dist.broadcast_object_list(box, src=0)
+    # torchrun's elastic variables (TORCHELASTIC_USE_AGENT_STORE, ...) would make the child's
+    # init_process_group a client of the agent's store instead of starting its own on the new port
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("TORCHELASTIC_", "TORCH_ELASTIC_"))}
+    env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(box[0]))
+    transport = os.environ.get("DSE_PARTITIONED_TRANSPORT", "rccl")
+    if cmd is None:
+        n_sea = os.environ.get("DSE_PARTITIONED_NSEA", "29")  # smaller registers only in a rehearsal
+        cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "bench_partitioned.py"), "--n-sea", n_sea,
+               "--t-final", "5e-6", "--steps", "6", "--transport", transport]
+    dist.barrier()
+    note(f"rank {rank}: partitioned leg child started ({' '.join(cmd[2:])})")
+    t0 = time.perf_counter()
+    try:
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        rc, out, err = res.returncode, res.stdout, res.stderr
+    except subprocess.TimeoutExpired as exc:
+        rc, out, err = "timeout", exc.stdout or "", exc.stderr or ""
+        out = out.decode() if isinstance(out, bytes) else out
+        err = err.decode() if isinstance(err, bytes) else err
+    wall = time.perf_counter() - t0
+    note(f"rank {rank}: partitioned leg child ended rc={rc} after {wall:.1f} s")
+    if rank != 0:
+        return {}
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if rc == 0 and lines:
+        rep = json.loads(lines[-1])
+        rep["child_wall_s"] = wall
+        return rep
+    return {"error": f"child rc={rc}", "child_wall_s": wall, "stderr_tail": err[-1500:]}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -256,12 +313,17 @@ def main():
         except Exception as exc:  # report, never hide
             cpu = {"value": None, "error": repr(exc)}
     import torch
+    local = local % max(torch.cuda.device_count(), 1)  # several ranks per GPU only in a rehearsal
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         # RCCL carries only the barrier and the max-time reduction: the evolutions are independent
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("DSE_BENCH_BACKEND", "nccl")  # gloo: a rehearsal on one GPU
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
 
     from quantumsimulations_amd import problem as pb
     from quantumsimulations_amd.engine import Engine
@@ -272,6 +334,8 @@ def main():
     probs = [pb.build_problem(p) for p in params]
     t = np.linspace(0.0, T_FINAL, STEPS_T)
 
+    if world > 1:
+        note(f"rank {rank}/{world}: device {local}, {len(probs)} evolutions")
     eng = Engine(local, tile_bits=args.tile_bits)
     eng.set_option("streams", args.streams)
     eng.set_option("persistent", 0 if args.streaming else 1)
@@ -292,6 +356,8 @@ def main():
             stats.append(st)
     dt = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, dist)
 
+    if world > 1:
+        note(f"rank {rank}: timed steps done ({dt:.3f} s)")
     points = len(my_det) * world * args.steps
     value = points / dt * 3600.0
     h_apps = sum(s["h_applications"] for s in stats)
@@ -394,6 +460,14 @@ def main():
             line["large_register"] = large_register(local)
         except Exception as exc:  # report, never hide
             line["large_register"] = {"error": repr(exc)}
+    if world in (2, 4, 8) and not args.no_large:
+        try:
+            rep = partitioned_leg(rank, world, int(os.environ.get("LOCAL_RANK", "0")), dist,
+                                  args.partitioned_timeout)
+        except Exception as exc:  # report, never hide
+            rep = {"error": repr(exc)}
+        if rank == 0:
+            line["partitioned"] = rep
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -3,6 +3,7 @@ of the bench's sharding + max-over-ranks timing, and the sweep dispatcher's per-
 a stand-in engine (no GPU here; the real engine is exercised by the -m gpu tests)."""
 import os
 import socket
+import sys
 import time
 
 import numpy as np
@@ -35,6 +36,44 @@ def _worker(rank, world, port, out):
     dt = bench.timed_steps(step, steps=3, warmup=1, sync=lambda: None, dist=dist)
     out[rank] = (det.tolist(), dt, n_calls[0])
     dist.destroy_process_group()
+
+
+def _partitioned_worker(rank, world, port, child, timeout, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ["TORCHELASTIC_USE_AGENT_STORE"] = "True"   # as under torchrun: must not reach the child
+    t0 = time.perf_counter()
+    rep = bench.partitioned_leg(rank, world, rank, dist, timeout, cmd=[sys.executable, "-c", child])
+    out[rank] = (rep, time.perf_counter() - t0)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["ok", "hang", "crash"])
+def test_bench_partitioned_leg_plumbing_gloo(case):
+    """bench.py's N > 1 config-5 leg: one child per rank on a fresh bootstrap port, rank 0 reports
+    its child's JSON line; a hung child is killed at the timeout and a failing one reported, both
+    without raising (the sweep's measurement is never lost to the extra leg)."""
+    child = {
+        "ok": ("import json, os; r = int(os.environ['RANK']); w = int(os.environ['WORLD_SIZE']); "
+               "assert os.environ['MASTER_PORT'] and 'TORCHELASTIC_USE_AGENT_STORE' not in os.environ; "
+               "r == 0 and print(json.dumps({'world': w, 'ok': True}))"),
+        "hang": "import time; time.sleep(60)",
+        "crash": "import sys; sys.stderr.write('boom'); sys.exit(3)",
+    }[case]
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_partitioned_worker, args=(world, _free_port(), child, 3.0, out), nprocs=world, join=True)
+    rep0, wall0 = out[0]
+    assert out[1][0] == {}
+    if case == "ok":
+        assert rep0["world"] == 2 and rep0["ok"] is True and rep0["child_wall_s"] < 30
+    else:
+        assert "error" in rep0 and wall0 < 30
+        assert ("timeout" in rep0["error"]) == (case == "hang")
+        if case == "crash":
+            assert "boom" in rep0["stderr_tail"]
 
 
 def test_bench_sharding_and_timing_gloo():

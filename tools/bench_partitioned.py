@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--delta", type=float, default=50e3)
     ap.add_argument("--loopback", type=int, default=0, help="all shards on one GPU (2, 4 or 8)")
     ap.add_argument("--wht", type=int, default=1)
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                    help="rccl: libdse's RCCL communicator (one GPU per rank); host: the library's host "
+                         "exchange backend over torch.distributed gloo (several ranks may share a GPU)")
     a = ap.parse_args()
     p = sweep_point_params(a.n_sea, a.delta, "center_on", a.t_final, a.steps)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -58,12 +61,18 @@ def main():
     else:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("gloo")       # bootstrap only; the data path is RCCL in libdse
-        with Engine(local) as eng:
+        dev = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo")       # bootstrap (rccl) or the data path itself (host)
+        with Engine(dev) as eng:
             eng.set_option("wht", a.wht)
-            join(eng, rank, world, dist)
+            if a.transport == "rccl":
+                join(eng, rank, world, dist)
+            else:
+                eng.dist_init_exchange(rank, world, dist)
             dist.barrier()
+            print(f"[bench_partitioned] rank {rank}/{world} joined ({a.transport}), N={prob.n_qubits}",
+                  file=sys.stderr, flush=True)
             t0 = time.perf_counter()
             _, obs, st = simulate_rare_partitioned(p, eng, rank, world)
             wall = time.perf_counter() - t0
@@ -71,7 +80,8 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             wall = float(tt.item())
         obs_d = {k: float(v[-1]) for k, v in obs.items()}
-        shards, mode = world, "RCCL send/recv between ranks"
+        shards = world
+        mode = "RCCL between ranks" if a.transport == "rccl" else "host exchange over gloo"
         dist.destroy_process_group()
     n = prob.n_qubits
     bits = shard_bits_for(shards)
@@ -107,6 +117,9 @@ def main():
             # per-link rate while the exchange runs (the passes run between exchanges)
             "xgmi_gbs_per_link_lower_bound": (measured / links / wall / 1e9) if not a.loopback else None,
             "obs_t_final": obs_d,
+            # exact propagation conserves the norm: the end-to-end check of the exchanged path
+            "norm_error": abs(obs_d["state_norm"] - 1.0),
+            "ok": bool(abs(obs_d["state_norm"] - 1.0) < 1e-9),
         }), flush=True)
 
 
