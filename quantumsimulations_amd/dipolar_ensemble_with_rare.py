@@ -78,11 +78,9 @@ def simulate_rare_batch(params_list: Sequence[DipolarRareParams], device: int | 
     probs = [build_problem(p, order="engine", reduce=True) for p in params_list]
     eng = _engine(device)
     results: List = [None] * len(params_list)
-    # one engine call per distinct time grid
-    by_grid: Dict[Tuple[float, int], List[int]] = {}
-    for i, p in enumerate(params_list):
-        by_grid.setdefault((float(p.t_final), int(p.steps)), []).append(i)
-    from .engine import batches_for_memory
+    # one engine call per distinct time grid and engine class (engine.evolve_groups)
+    from .engine import batches_for_memory, evolve_groups
+    by_grid = evolve_groups([(float(p.t_final), int(p.steps)) for p in params_list], probs)
     for key, idxs in by_grid.items():
         for batch in batches_for_memory([probs[i] for i in idxs], device):
             members = [idxs[b] for b in batch]

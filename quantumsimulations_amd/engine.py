@@ -39,6 +39,26 @@ def problem_bytes(prob: Problem) -> float:
     return 16.0 * (3 + 1 + 2) * (1 << prob.n_qubits) + (4 << 20)
 
 
+# A libdse evolve runs its persistent interval kernel only when every register that is not on the
+# small-register engine fits one or two 2^13-amplitude tiles (dse_runtime.hip, dse_evolve's mode
+# choice); one larger register in the call drops all of them to the streaming kernels.
+PERSISTENT_MAX_QUBITS = 14
+
+
+def engine_class(prob: Problem) -> int:
+    """0: a register the persistent kernel (or the small-register engine) takes, 1: a larger one."""
+    return 0 if prob.n_qubits <= PERSISTENT_MAX_QUBITS else 1
+
+
+def evolve_groups(grid_keys, probs) -> Dict[Tuple, list]:
+    """Indices of problems that share one evolve call: the same time grid and the same engine
+    class, so a mixed batch keeps its tile-sized registers on the persistent kernel."""
+    groups: Dict[Tuple, list] = {}
+    for i, (key, p) in enumerate(zip(grid_keys, probs)):
+        groups.setdefault((*key, engine_class(p)), []).append(i)
+    return groups
+
+
 def batches_for_memory(probs, device: int, headroom: float = 0.8):
     """Index batches of ``probs`` whose summed footprint fits ``headroom`` of the free memory of
     ``device`` (at least one problem per batch; a problem too large alone still gets its own)."""

@@ -87,14 +87,14 @@ def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequ
     errors: List[BaseException] = []
 
     def work(dev: int, idxs: List[int]) -> None:
-        from .engine import Engine, batches_for_memory
+        from .engine import Engine, batches_for_memory, evolve_groups
         try:
             with Engine(dev) as eng:
-                by_grid: Dict[Tuple[float, int], List[int]] = {}
-                for i in idxs:
-                    by_grid.setdefault((float(params_list[i].t_final), int(params_list[i].steps)),
-                                       []).append(i)
-                for group in by_grid.values():
+                # one evolve per time grid and engine class, within the device's memory
+                sub = evolve_groups([(float(params_list[i].t_final), int(params_list[i].steps))
+                                     for i in idxs], [probs[i] for i in idxs])
+                for local in sub.values():
+                    group = [idxs[j] for j in local]
                     eng.clear()
                     for batch in batches_for_memory([probs[i] for i in group], dev):
                         eng.clear()

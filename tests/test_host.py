@@ -324,3 +324,17 @@ def test_run_reference_launcher_resolves_the_drop_in(tmp_path):
     assert res.returncode == 0, res.stderr[-2000:]
     assert res.stdout.split()[0] == "quantumsimulations_amd.dipolar_ensemble_with_rare"
     assert "'--x', '1'" in res.stdout
+
+
+def test_evolve_groups_split_by_engine_class():
+    """A batch mixing tile-sized (N <= 14) and larger registers is split so the tile-sized ones
+    keep the persistent interval kernel (one larger register would demote the whole evolve)."""
+    from types import SimpleNamespace
+
+    from quantumsimulations_amd.engine import engine_class, evolve_groups
+
+    probs = [SimpleNamespace(n_qubits=n) for n in (7, 14, 16, 13, 30, 14)]
+    keys = [(1e-3, 101)] * 5 + [(2e-3, 101)]
+    assert [engine_class(p) for p in probs] == [0, 0, 1, 0, 1, 0]
+    g = evolve_groups(keys, probs)
+    assert g == {(1e-3, 101, 0): [0, 1, 3], (1e-3, 101, 1): [2, 4], (2e-3, 101, 0): [5]}
