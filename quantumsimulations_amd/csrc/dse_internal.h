@@ -21,6 +21,9 @@ __host__ __device__ constexpr int rr_index(int a, int b) {
 }
 constexpr int kXSlots = 4;                        // hand-off ring of the interval kernel
 constexpr int kIvWaves = 8;                       // hand-off flags per tile (one per wave of a 2^13 tile)
+#ifndef DSE_PIPE
+#define DSE_PIPE 1  // interval kernel: software-pipelined partner reads in the fused loop
+#endif
 #ifndef DSE_MAX_OUT
 #define DSE_MAX_OUT 2
 #endif

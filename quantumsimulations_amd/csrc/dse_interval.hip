@@ -90,6 +90,36 @@ __device__ __forceinline__ void rmad(double2& acc, double g, double2 s) {
   acc.y = fma(g, s.y, acc.y);
 }
 
+typedef __attribute__((address_space(3))) const dv2 ldv2;
+
+// LDS byte address of a __shared__ object (for the half-tile row reads below)
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(const T* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) T*)p;
+}
+
+// Rows hh * NH + r0 .. hh * NH + r0 + NR - 1 of thread t from the LDS tile w (row r of thread t
+// at w[r * NT + t]).  One base address per half and the rows at immediate offsets: the second half
+// of a 2^13 tile starts 64 KiB in, past ds_read's 16-bit offset field, and left to itself the
+// compiler forms one address per row (8 extra VALU adds per partner half).  The base of the
+// second half is made opaque so it is not re-associated into per-row adds.
+template <int NT, int NH, int NR>
+__device__ __forceinline__ void ld_rows(const double2* w, int t, int hh, int r0, double2* v) {
+  uint32_t a = lds_addr(w + t);
+  constexpr uint32_t HALF = (uint32_t)NH * NT * 16u;
+  if (hh) {
+    if (HALF >= 65536u)
+      asm("v_add_u32_e32 %0, %1, %2" : "=v"(a) : "i"(HALF), "v"(a));
+    else
+      a += HALF;
+  }
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) {
+    const dv2 d = *(ldv2*)(size_t)(a + (uint32_t)(r0 + rr) * NT * 16u);
+    v[rr] = make_double2(d.x, d.y);
+  }
+}
+
 template <int L>
 struct IvShared {
   double2 w[RB<L>::T];  // the tile of w_{k-1}
@@ -98,10 +128,14 @@ struct IvShared {
   double zr[kRegAmps];  // register-bit ZZ part of the diagonal per r
   // per-thread diagonal D(r) = td[0] + sum_i td[1 + i] s_i(r) + zr[r], kept here rather than in
   // registers: the kernel is at the 256-VGPR limit and these are read once per term
-  double td[1 + kRegBits][RB<L>::NT];
+  // (pairs per thread: {td0, td1}, {td2, td3}, {td4, 0} -- addressed like the tile rows, from the
+  // thread's 16-byte index, so no separate address register stays live across the term)
+  dv2 td[3][RB<L>::NT];
   double xg[kRegBits];  // cross pairs (register bit i, top bit) of the u pre-pass
-  DSweep sw[RB<L>::TB];        // thread-bit sweeps (LDS copies of P.sweeps: counted waits, no SMEM)
-  DPair tt[4 * RB<L>::TB];     // thread-bit pairs, zero-padded to four per sweep
+  // per fused-loop iteration j (thread bit j), 8 granules: the first 64 B of P.sweeps[j] (re0 im0 |
+  // re1 im1 | g0 g1 | g2 g3) and thread pairs 4j .. 4j + 3 of P.pairs_tt (mask_lo tile_xor | g),
+  // zero past the list -- LDS copies (counted waits, no SMEM), one base address per iteration
+  dv2 it[RB<L>::TB][8];
 };
 
 template <int L, bool IMAG>
@@ -109,6 +143,9 @@ __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
            int n_out, int* __restrict__ flags, int* __restrict__ err) {
   constexpr int NT = RB<L>::NT, R = kRegAmps, TB = RB<L>::TB, NH = R / 2;
+  // software-pipelined partner reads in the fused loop (the production IMAG build; the general
+  // build keeps the plain order, which fits its larger drive arithmetic without spilling)
+  constexpr bool PIPE = DSE_PIPE && IMAG;
   constexpr uint32_t T = 1u << L;
   __shared__ IvShared<L> S;
   __shared__ int s_fail;
@@ -152,9 +189,8 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) dj[j] = j < n_out ? (int)crow[j * rstride] : 0;
 
-  // diagnostics only (0 in production): 1 skip the sweeps, 2 skip the thread-bit pairs, 4 skip
-  // the register-bit terms, 64 skip the hand-off stores and flag, 128 skip the partner wait and
-  // read, 256 skip the acc updates, 512 skip the tile terms
+  // diagnostics only (0 in production): 4 skip the register-bit terms, 64 skip the hand-off stores
+  // and flag, 128 skip the partner wait and read, 256 skip the acc updates, 512 skip the tile terms
   const int ab = g_dse_ablate_iv;
   const bool fences = g_dse_handoff_fences != 0;
 
@@ -168,13 +204,18 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       S.zz[e] = (j > i) ? zz[i * n + j] : 0.0;
     }
     tile_diag_coeffs<L>(P, h, P.beta, S.c, tid);
-    stage16(S.sw, P.sweeps, TB * (int)(sizeof(DSweep) / 16), tid, NT);
+    static_assert(sizeof(DSweep) == 80 && sizeof(DPair) == 16, "iteration table layout");
+    const gd2* psw = (const gd2*)P.sweeps;
     const gd2* ptt = (const gd2*)P.pairs_tt;
-    for (int e = tid; e < 4 * TB; e += NT) {  // DPair is one 16-byte granule; zero past the list
+    for (int e = tid; e < 8 * TB; e += NT) {
+      const int j = e >> 3, c = e & 7;
       dv2 v;
       v.x = v.y = 0.0;
-      if (e < P.n_pairs_tt) v = ptt[e];
-      reinterpret_cast<dv2*>(S.tt)[e] = v;
+      if (c < 4)
+        v = psw[j * 5 + c];
+      else if (4 * j + c - 4 < P.n_pairs_tt)
+        v = ptt[4 * j + c - 4];
+      S.it[j][c] = v;
     }
   }
 #pragma unroll
@@ -202,9 +243,16 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
     for (int i = 0; i < kRegBits; ++i) hr[i] += S.zz[j * L + TB + i] * sj;
   }
-  S.td[0][tid] = zt;
-#pragma unroll
-  for (int i = 0; i < kRegBits; ++i) S.td[1 + i][tid] = hr[i];
+  static_assert(kRegBits == 4, "td packing");
+  {
+    dv2 v;
+    v.x = zt, v.y = hr[0];
+    S.td[0][tid] = v;
+    v.x = hr[1], v.y = hr[2];
+    S.td[1][tid] = v;
+    v.x = hr[3], v.y = 0.0;
+    S.td[2][tid] = v;
+  }
   // register-bit cross pairs (register bit i, top bit) for the u pre-pass
   if (tid < kRegBits) {
     double g = 0.0;
@@ -228,8 +276,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         double2 ow[NH];
-#pragma unroll
-        for (int rr = 0; rr < NH; ++rr) ow[rr] = S.w[(hh * NH + rr) * NT + tid];
+        ld_rows<NT, NH, NH>(S.w, tid, hh, 0, ow);
         for (int f = 0; f < P.n_flips_hi; ++f) {  // top-bit drive at the partner's bit value
           const double cr = b_pa ? cfh[f].re1 : cfh[f].re0, ci = b_pa ? cfh[f].im1 : cfh[f].im0;
 #pragma unroll
@@ -259,8 +306,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           double2 pv[NH];
-#pragma unroll
-          for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+          ld_rows<NT, NH, NH>(S.w, pt, hh, 0, pv);
 #pragma unroll
           for (int rr = 0; rr < NH; ++rr) rmad(u[hh * NH + rr], g, pv[rr]);
         }
@@ -280,11 +326,13 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
         for (int r = 0; r < R; ++r) out[r] = own[r];
       } else {
+        const dv2 t01 = S.td[0][tid], t23 = S.td[1][tid], t4 = S.td[2][tid];
+        const double tdv[1 + kRegBits] = {t01.x, t01.y, t23.x, t23.y, t4.x};
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          double d = S.td[0][tid] + S.zr[r];
+          double d = tdv[0] + S.zr[r];
 #pragma unroll
-          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * S.td[1 + i][tid];
+          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * tdv[1 + i];
           out[r].x = d * own[r].x;
           out[r].y = d * own[r].y;
         }
@@ -343,49 +391,96 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll 1
     for (int j = 0; j < ((ab & 512) ? 0 : TB); ++j) {
       if (j == J_PUB) publish();
-      const DSweep sw = S.sw[j];
-      const int bj = (tid >> j) & 1;
       const int pt = tid ^ (1 << j);
-      const double sk = (ab & 1) ? 0.0 : 1.0;
-      const double cr = sk * (bj ? sw.re1 : sw.re0), ci = sk * (bj ? sw.im1 : sw.im0);
+      double2 pv[NH];  // partner rows of the sweep (PIPE: the first half, in flight under the tables)
+      if constexpr (PIPE) ld_rows<NT, NH, NH>(S.w, pt, 0, 0, pv);
+      // the iteration's tables (S.it[j]), eight 16-byte reads issued together
+      dv2 swv[4], ttv[4];
+      {
+        // one VGPR base for the eight reads (immediate offsets); left uniform, the compiler forms
+        // each address in an SGPR and moves it into one reused VGPR, serialising the reads
+        uint32_t ia;
+        asm("v_mov_b32_e32 %0, %1" : "=v"(ia) : "s"(lds_addr(&S.it[j][0])));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) swv[e] = *(ldv2*)(size_t)(ia + 16u * e);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ttv[e] = *(ldv2*)(size_t)(ia + 16u * (4 + e));
+      }
+      const int bj = (tid >> j) & 1;
+      const double cr = bj ? swv[1].x : swv[0].x, ci = bj ? swv[1].y : swv[0].y;
       double g0[kRegBits], g1[kRegBits];  // pair (j, register bit i) on rows with r_i = 0 / 1
 #pragma unroll
       for (int i = 0; i < kRegBits; ++i) {
-        g0[i] = bj ? 0.0 : sk * sw.g[i];
-        g1[i] = bj ? sk * sw.g[i] : 0.0;
+        const double g = (i & 1) ? swv[2 + i / 2].y : swv[2 + i / 2].x;
+        g0[i] = bj ? 0.0 : g;
+        g1[i] = bj ? g : 0.0;
       }
       int tpt[4];
       double ge[4];
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const DPair e = S.tt[4 * j + qq];  // zero entries beyond the problem's pairs
-        tpt[qq] = tid ^ (int)e.mask_lo;
-        ge[qq] = (par32((uint32_t)tid & e.mask_lo) || (ab & 2)) ? 0.0 : e.g;  // rows with x_i == x_j
+      for (int qq = 0; qq < 4; ++qq) {  // zero entries beyond the problem's pairs
+        const uint32_t m = (uint32_t)__double_as_longlong(ttv[qq].x);  // DPair::mask_lo
+        tpt[qq] = tid ^ (int)m;
+        ge[qq] = par32((uint32_t)tid & m) ? 0.0 : ttv[qq].y;  // rows with x_i == x_j
       }
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        double2 pv[NH];
-#pragma unroll
-        for (int rr = 0; rr < NH; ++rr) pv[rr] = S.w[(hh * NH + rr) * NT + pt];
+      auto gsel = [&](int i, int bit) { return bit ? g1[i] : g0[i]; };
+      // the sweep of half hh (rows r_3 = hh) from the partner rows pv, and thread pair qq on half hh
+      auto sweep = [&](int hh, const double2* pv) {
         double2* oh = out + hh * NH;
 #pragma unroll
         for (int rr = 0; rr < NH; ++rr) oh[rr] = dmad<IMAG>(oh[rr], cr, ci, pv[rr]);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ((rr >> i) & 1) ? g1[i] : g0[i], pv[rr ^ (1 << i)]);
+          for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], gsel(i, (rr >> i) & 1), pv[rr ^ (1 << i)]);
         // (j, register bit 3): rows of the other half, r_3 = 1 - hh
         double2* oo = out + (1 - hh) * NH;
-        const double g3 = hh ? g0[3] : g1[3];
+        const double g3 = gsel(3, 1 - hh);
 #pragma unroll
         for (int rr = 0; rr < NH; ++rr) rmad(oo[rr], g3, pv[rr]);
+      };
+      auto tpair = [&](int qq, int hh, const double2* tv) {
+        double2* oh = out + hh * NH;
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          double2 tv[NH];
+        for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ge[qq], tv[rr]);
+      };
+      if constexpr (PIPE) {
+        // software pipeline over the iteration's partner reads: the sweep's 8-row halves and the
+        // thread pairs in 4-row quarters, each next read issued before the FMAs of the current one
+        // (+2-3% points/h, profiles/r02/ab/pipelined_loop.jsonl)
+        constexpr int NQ = NH / 2;
+        auto tpair_q = [&](int qq, int hh, int qh, const double2* tv) {
+          double2* oh = out + hh * NH + qh * NQ;
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) tv[rr] = S.w[(hh * NH + rr) * NT + tpt[qq]];
+          for (int rr = 0; rr < NQ; ++rr) rmad(oh[rr], ge[qq], tv[rr]);
+        };
+        double2 qa[NQ], qb[NQ];
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) rmad(oh[rr], ge[qq], tv[rr]);
+        for (int hh = 0; hh < 2; ++hh) {
+          ld_rows<NT, NH, NQ>(S.w, tpt[0], hh, 0, qa);
+          sweep(hh, pv);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            ld_rows<NT, NH, NQ>(S.w, tpt[qq], hh, NQ, qb);
+            tpair_q(qq, hh, 0, qa);
+            if (qq < 3)
+              ld_rows<NT, NH, NQ>(S.w, tpt[qq + 1], hh, 0, qa);
+            else if (hh == 0)
+              ld_rows<NT, NH, NH>(S.w, pt, 1, 0, pv);
+            tpair_q(qq, hh, 1, qb);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          ld_rows<NT, NH, NH>(S.w, pt, hh, 0, pv);
+          sweep(hh, pv);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            double2 tv[NH];
+            ld_rows<NT, NH, NH>(S.w, tpt[qq], hh, 0, tv);
+            tpair(qq, hh, tv);
+          }
         }
       }
     }

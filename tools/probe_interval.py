@@ -62,8 +62,7 @@ def main():
     for which in sets:
         for name, mask in (("full", 0), ("no_publish", 64), ("no_wait_read", 128),
                            ("no_exchange", 64 | 128), ("no_acc", 256), ("no_tile_terms", 512),
-                           ("exchange_only", 256 | 512), ("no_sweeps", 1), ("no_tt_pairs", 2),
-                           ("no_register_terms", 4), ("register_terms_only", 1 | 2)):
+                           ("exchange_only", 256 | 512), ("no_register_terms", 4)):
             if which in ("singles", "all") and mask & (64 | 128):
                 continue
             ms, st = run(eng, probs, t, mask, which)
