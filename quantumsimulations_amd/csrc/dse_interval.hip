@@ -40,6 +40,8 @@
 // Register budget: this kernel must not spill VGPRs.  A build that spilled 12 VGPRs (stored once in
 // the prologue, reloaded every term) gave run-to-run differences of ~1e-9 on 2-tile problems;
 // tests/test_build.py checks the resource usage and tests/test_gpu_parity.py bitwise determinism.
+#include <type_traits>
+
 #include "dse_device.h"
 
 namespace dse {
@@ -267,7 +269,63 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
   for (int r = 0; r < R; ++r) prev[r] = make_double2(0.0, 0.0);
 
+  // The term loop is instantiated twice, for tiles with and without the u pre-pass (crossing pairs),
+  // so that the register allocator sees the two phase orders separately (block-uniform dispatch).
+  auto term_loop = [&](auto xg_tag) {
+  constexpr bool xgen = decltype(xg_tag)::value;
+  const bool xraw = pair && !xgen;
   for (int k = 1; k <= K; ++k) {
+    // ---- phase 1: diagonal and register-bit terms (the thread's own rows, which it wrote itself).
+    // Without a pre-pass it runs before the barrier, while the other threads' stores of w_{k-1}
+    // to LDS drain; with one, after the pre-pass, whose u does not fit beside out ----
+    double2 out[R];
+    auto phase1 = [&]() {
+      double2 own[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) own[r] = S.w[r * NT + tid];
+      if (ab & (512 | 4)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) out[r] = own[r];
+      } else {
+        const dv2 t01 = S.td[0][tid], t23 = S.td[1][tid], t4 = S.td[2][tid];
+        const double tdv[1 + kRegBits] = {t01.x, t01.y, t23.x, t23.y, t4.x};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          double d = tdv[0] + S.zr[r];
+#pragma unroll
+          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * tdv[1 + i];
+          out[r].x = d * own[r].x;
+          out[r].y = d * own[r].y;
+        }
+        if (P.rflip_mask) {
+#pragma unroll
+          for (int i = 0; i < kRegBits; ++i) {
+            if (!((P.rflip_mask >> i) & 1)) continue;
+            const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const bool v = (r >> i) & 1;
+              out[r] = dmad<IMAG>(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
+            }
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < kRegBits; ++a)
+#pragma unroll
+          for (int b = a + 1; b < kRegBits; ++b) {
+            const double g = P.rr_g[rr_index(a, b)];
+            if (g == 0.0) continue;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
+              rmad(out[r], g, own[r ^ ((1 << a) | (1 << b))]);
+            }
+          }
+      }
+    };
+    if constexpr (!xgen) phase1();
+    __syncthreads();  // w_{k-1} complete in LDS
+
     // ---- phase 0 (crossing pairs): u(w_{k-1}) for the partner -> slot (k-1)&1, sc1 ----
     if (xgen && !(ab & 64)) {
       double2 u[R];
@@ -316,52 +374,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), u[r]);
     }
 
-    // ---- phase 1: diagonal and register-bit terms ----
-    double2 out[R];
-    {
-      double2 own[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) own[r] = S.w[r * NT + tid];
-      if (ab & (512 | 4)) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) out[r] = own[r];
-      } else {
-        const dv2 t01 = S.td[0][tid], t23 = S.td[1][tid], t4 = S.td[2][tid];
-        const double tdv[1 + kRegBits] = {t01.x, t01.y, t23.x, t23.y, t4.x};
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          double d = tdv[0] + S.zr[r];
-#pragma unroll
-          for (int i = 0; i < kRegBits; ++i) d += ((r >> i) & 1 ? -0.5 : 0.5) * tdv[1 + i];
-          out[r].x = d * own[r].x;
-          out[r].y = d * own[r].y;
-        }
-        if (P.rflip_mask) {
-#pragma unroll
-          for (int i = 0; i < kRegBits; ++i) {
-            if (!((P.rflip_mask >> i) & 1)) continue;
-            const double c0r = P.rflip[i][0], c0i = P.rflip[i][1], c1r = P.rflip[i][2], c1i = P.rflip[i][3];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-              const bool v = (r >> i) & 1;
-              out[r] = dmad<IMAG>(out[r], v ? c1r : c0r, v ? c1i : c0i, own[r ^ (1 << i)]);
-            }
-          }
-        }
-#pragma unroll
-        for (int a = 0; a < kRegBits; ++a)
-#pragma unroll
-          for (int b = a + 1; b < kRegBits; ++b) {
-            const double g = P.rr_g[rr_index(a, b)];
-            if (g == 0.0) continue;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-              if (((r >> a) ^ (r >> b)) & 1) continue;  // compile-time after unrolling
-              rmad(out[r], g, own[r ^ ((1 << a) | (1 << b))]);
-            }
-          }
-      }
-    }
+    if constexpr (xgen) phase1();
 
     // ---- publish (per wave): thread t's hand-off rows are read only by thread t of the partner
     // tile, i.e. wave w's stores only by the partner's wave w.  The wave waits for its own stores
@@ -585,6 +598,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       for (int r = 0; r < AB; ++r) prev[r0 + r] = ownb[r];
     }
     __syncthreads();  // every read of w_{k-1} in LDS is done
+    if (s_fail) break;  // uniform: a hand-off timed out (error reported to the host)
 #pragma unroll
     for (int r = 0; r < R; ++r) S.w[r * NT + tid] = out[r];
     if (xraw && k < K && !(ab & 64)) {  // w_k for the partner's term k + 1
@@ -592,9 +606,12 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
 #pragma unroll
       for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), out[r]);
     }
-    __syncthreads();
-    if (s_fail) break;  // uniform: a hand-off timed out (error reported to the host)
   }
+  };
+  if (xgen)
+    term_loop(std::true_type{});
+  else
+    term_loop(std::false_type{});
 }
 
 // hand-off flags of the launched items only (2 per problem: flags[2 * problem + tile]), so the
