@@ -134,6 +134,7 @@ struct IvShared {
   // thread's 16-byte index, so no separate address register stays live across the term)
   dv2 td[3][RB<L>::NT];
   double xg[kRegBits];  // cross pairs (register bit i, top bit) of the u pre-pass
+  double xq[RB<L>::TB];  // cross pairs (thread bit j, top bit) of the u pre-pass (0: none)
   // per fused-loop iteration j (thread bit j), 8 granules: the first 64 B of P.sweeps[j] (re0 im0 |
   // re1 im1 | g0 g1 | g2 g3) and thread pairs 4j .. 4j + 3 of P.pairs_tt (mask_lo tile_xor | g),
   // zero past the list -- LDS copies (counted waits, no SMEM), one base address per iteration
@@ -263,6 +264,13 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
         if (cph[p].mask_lo == (1u << (TB + tid))) g = cph[p].g;
     S.xg[tid] = g;
   }
+  if (tid < TB) {
+    double g = 0.0;
+    if (xgen)
+      for (int p = 0; p < P.n_pairs_hi; ++p)
+        if (cph[p].mask_lo == (1u << tid)) g = cph[p].g;
+    S.xq[tid] = g;
+  }
   __syncthreads();
 
   double2 prev[R];
@@ -354,20 +362,20 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
           for (int rr = 0; rr < NH; ++rr) rmad(u[(1 - hh) * NH + rr], g, ow[rr]);
         }
       }
-      // (thread bit j, top): applies iff t_j == b_pa, source t ^ e_j
-      for (int p = 0; p < P.n_pairs_hi; ++p) {
-        const uint32_t m = cph[p].mask_lo;
-        if (m >= (1u << TB)) continue;
-        if ((((uint32_t)tid & m) != 0u) != (b_pa != 0u)) continue;
-        const double g = cph[p].g;
-        const int pt = tid ^ (int)m;
+      // (thread bit j, top): applies iff t_j == b_pa, source t ^ e_j.  All nine thread bits in a
+      // software pipeline of 8-row halves (the next half in flight under the current FMAs), the
+      // coefficient zero in the lanes where the pair does not act
+      double2 ba[NH], bb[NH];
+      ld_rows<NT, NH, NH>(S.w, tid ^ 1, 0, 0, ba);
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          double2 pv[NH];
-          ld_rows<NT, NH, NH>(S.w, pt, hh, 0, pv);
+      for (int j = 0; j < TB; ++j) {
+        const double gj = ((uint32_t)((tid >> j) & 1) == b_pa) ? S.xq[j] : 0.0;
+        ld_rows<NT, NH, NH>(S.w, tid ^ (1 << j), 1, 0, bb);
 #pragma unroll
-          for (int rr = 0; rr < NH; ++rr) rmad(u[hh * NH + rr], g, pv[rr]);
-        }
+        for (int rr = 0; rr < NH; ++rr) rmad(u[rr], gj, ba[rr]);
+        if (j + 1 < TB) ld_rows<NT, NH, NH>(S.w, tid ^ (1 << (j + 1)), 0, 0, ba);
+#pragma unroll
+        for (int rr = 0; rr < NH; ++rr) rmad(u[NH + rr], gj, bb[rr]);
       }
       const __amdgpu_buffer_rsrc_t dst = tile_rsrc(xs_me + ((size_t)((k - 1) % kXSlots) << L), TBYTES);
 #pragma unroll

@@ -16,5 +16,5 @@ for i in 1 2; do
     python -c "import json; d=json.load(open('$OUT/ab_$v$i.json')); r=d['roofline']; print(json.dumps({'variant':'$v','value':round(d['value']),'ms_per_step':round(d['ms_per_step'],1),'frac':round(r['frac'],3),'avg_launch_us':round(r['avg_launch_us'],1),'chip_frac':round(r['chip_level']['frac'],3)}))" | tee -a $OUT/ab.jsonl || exit 1
   done
 done
-DSE_LIB=quantumsimulations_amd/libdse.so timeout -k 10 300 python -u tools/probe_interval.py > $OUT/probe.jsonl 2> $OUT/probe.err
+DSE_LIB=quantumsimulations_amd/libdse.so timeout -k 10 300 python -u tools/probe_interval.py center_on,shell_off,pairs,singles > $OUT/probe.jsonl 2> $OUT/probe.err
 exit 0
