@@ -131,6 +131,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         13)
  *          "wht_group_bits"  high qubits transformed per pass of that engine, 2..11, or 0
  *                         (default: tile bits - 2)
+ *          "swap_overlap" partitioned registers on that engine: 1 (default) the X- and Y-branch
+ *                         vectors take separate passes and each one's index swap runs on a
+ *                         second stream under the other's pass; 0: both swapped between passes
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
  *          "max_degree"   Chebyshev degree cap per interval (default 2e6)

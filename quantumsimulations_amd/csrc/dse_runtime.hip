@@ -156,6 +156,11 @@ struct dse_ctx {
   int small = 1;                    // registers of <= 9 qubits run on dse_small.hip
   int small_chunk = 64;             // output intervals per launch of that engine
   hipStream_t small_stream = nullptr;
+  // partitioned registers on the Walsh-Hadamard engine: the index swaps run on swap_stream, one
+  // vector's swap under the other vector's pass (option "swap_overlap"); swap_ev orders the two
+  int swap_overlap = 1;
+  hipStream_t swap_stream = nullptr;
+  hipEvent_t swap_ev[8] = {};
   SmallProb* d_small = nullptr;
   size_t small_cap = 0;             // descriptors allocated
   double* d_small_out = nullptr;    // [problem][n_t][8] raw observable sums
@@ -280,6 +285,13 @@ void free_device(dse_ctx* ctx) {
 }
 
 void destroy_lanes(dse_ctx* ctx) {
+  if (ctx->swap_stream) {
+    (void)hipStreamSynchronize(ctx->swap_stream);
+    for (auto& e : ctx->swap_ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    (void)hipStreamDestroy(ctx->swap_stream);
+    ctx->swap_stream = nullptr;
+  }
   if (ctx->small_stream) {
     (void)hipStreamSynchronize(ctx->small_stream);
     (void)hipStreamDestroy(ctx->small_stream);
@@ -303,6 +315,7 @@ int ensure_lanes(dse_ctx* ctx) {
 }
 
 int sync_all(dse_ctx* ctx) {
+  if (ctx->swap_stream) HIPC(hipStreamSynchronize(ctx->swap_stream));
   for (auto& ln : ctx->lanes) HIPC(hipStreamSynchronize(ln.stream));
   if (ctx->small_stream) HIPC(hipStreamSynchronize(ctx->small_stream));
   return DSE_OK;
@@ -723,13 +736,14 @@ int xchg_allreduce_host(dse_ctx* ctx, double* v, size_t count, hipStream_t st) {
 // Index swap of the X/Y vectors of partitioned registers (local top S bits <-> shard bits):
 // chunk p of shard r -> chunk r of shard p; an involution, so back = the same exchange from the
 // swapped copies.  Loopback registers: device copies; one shard per process: RCCL all-to-all.
-int wht_swap(dse_ctx* ctx, const std::vector<int>& regs, bool back, hipStream_t st) {
+int wht_swap(dse_ctx* ctx, const std::vector<int>& regs, bool back, hipStream_t st, int vsel = 3) {
   for (int first : regs) {
     const HostProblem& P0 = ctx->probs[first];
     const int S = P0.shard_bits;
     const size_t chunk = size_t(1) << (P0.n_local - S);
     const size_t cbytes = chunk * sizeof(double2);
     for (int v = 0; v < 2; ++v) {
+      if (!((vsel >> v) & 1)) continue;
       if (P0.dist) {
         const double2* src = P0.wvec[back ? 2 + v : v];
         double2* dst = P0.wvec[back ? v : 2 + v];
@@ -756,12 +770,52 @@ int wht_swap(dse_ctx* ctx, const std::vector<int>& regs, bool back, hipStream_t 
 int wht_run(dse_ctx* ctx, int wl, int G, const std::vector<std::pair<const int2*, int>>& segs,
             const std::vector<int>& regs, int mode, int k, int q, int set, hipStream_t st) {
   int rc;
-  for (int part = WHT_PART_PRE; part <= WHT_PART_POST; ++part) {
-    if (part == WHT_PART_MID && !regs.empty() && (rc = wht_swap(ctx, regs, false, st))) return rc;
-    if (part == WHT_PART_POST && !regs.empty() && (rc = wht_swap(ctx, regs, true, st))) return rc;
+  auto part = [&](int pt, int vsel) -> int {
     for (const auto& sg : segs)
-      HIPC(launch_wht_part(part, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, st));
+      HIPC(launch_wht_part(pt, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, vsel, st));
+    return DSE_OK;
+  };
+  if (regs.empty() || !ctx->swap_overlap) {
+    for (int pt = WHT_PART_PRE; pt <= WHT_PART_POST; ++pt) {
+      if (pt == WHT_PART_MID && !regs.empty() && (rc = wht_swap(ctx, regs, false, st))) return rc;
+      if (pt == WHT_PART_POST && !regs.empty() && (rc = wht_swap(ctx, regs, true, st))) return rc;
+      if ((rc = part(pt, 3))) return rc;
+    }
+    return DSE_OK;
   }
+  // Partitioned registers: the X-branch vector A and the Y-branch vector B are transformed in
+  // separate launches, and each index swap (all-to-all over the shards) runs on swap_stream while
+  // the compute stream works on the other vector:
+  //   st    FIRST+FWD(A) | FWD(B) |        MID(A) |        MID(B) |        INV(A) |  INV(B)+FINAL
+  //   swap               | swap A | swap B        | back A        | back B
+  // ev[v]: vector v ready on st for its swap, ev[2+v]: swapped, ev[4+v]: MID done, ev[6+v]: back.
+  if (!ctx->swap_stream) {
+    HIPC(hipStreamCreateWithFlags(&ctx->swap_stream, hipStreamNonBlocking));
+    for (auto& e : ctx->swap_ev) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipStream_t sw = ctx->swap_stream;
+  hipEvent_t* ev = ctx->swap_ev;
+  // the swap stream takes over vector v once event i is reached on the compute stream, swaps it
+  // (there, or back), and marks event j when done
+  auto swap_after = [&](int i, int v, bool back, int j) -> int {
+    HIPC(hipEventRecord(ev[i], st));
+    HIPC(hipStreamWaitEvent(sw, ev[i], 0));
+    const int r = wht_swap(ctx, regs, back, sw, 1 << v);
+    if (r) return r;
+    HIPC(hipEventRecord(ev[j], sw));
+    return DSE_OK;
+  };
+  auto wait_swap = [&](int j) -> int {
+    HIPC(hipStreamWaitEvent(st, ev[j], 0));
+    return DSE_OK;
+  };
+  for (int v = 0; v < 2; ++v)  // PRE of A (with FIRST), then of B; each vector's swap behind it
+    if ((rc = part(WHT_PART_PRE, 1 << v)) || (rc = swap_after(v, v, false, 2 + v))) return rc;
+  for (int v = 0; v < 2; ++v)  // MID of a vector once it is swapped; its swap back behind it
+    if ((rc = wait_swap(2 + v)) || (rc = part(WHT_PART_MID, 1 << v)) || (rc = swap_after(4 + v, v, true, 6 + v)))
+      return rc;
+  for (int v = 0; v < 2; ++v)  // POST: INV(A), then INV(B) + FINAL
+    if ((rc = wait_swap(6 + v)) || (rc = part(WHT_PART_POST, 1 << v))) return rc;
   return DSE_OK;
 }
 
@@ -963,6 +1017,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     return ensure_lanes(ctx);
   } else if (k == "persistent") {
     ctx->persistent = value != 0.0;
+  } else if (k == "swap_overlap") {
+    ctx->swap_overlap = value != 0.0;
   } else if (k == "wht") {
     if ((value != 0.0) != (ctx->wht != 0)) {
       (void)sync_all(ctx);

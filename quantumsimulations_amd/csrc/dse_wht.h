@@ -60,9 +60,11 @@ hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64
 // roles and coefficient rows as launch_step) over items (problem, tile index), in three parts:
 //   pre  = FIRST, FWD over groups 1..G-2      mid = MID (group G-1)      post = INV, FINAL
 // (partitioned registers swap vec_* <-> vec_*t between the parts).  Every item's problem has
-// P.L == wl.
+// P.L == wl.  vsel selects the vectors (1: the X-branch A, 2: the Y-branch B, 3: both): pre with
+// vsel 1 = FIRST + FWD(A), 2 = FWD(B); mid = MID(vsel); post with vsel 1 = INV(A), 2 = INV(B) +
+// FINAL -- so a partitioned register can swap one vector while the other is transformed.
 enum { WHT_PART_PRE = 0, WHT_PART_MID = 1, WHT_PART_POST = 2 };
 hipError_t launch_wht_part(int part, int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
-                           const int2* items, int n_items, int k, int q, int set, hipStream_t st);
+                           const int2* items, int n_items, int k, int q, int set, int vsel, hipStream_t st);
 
 }  // namespace dse

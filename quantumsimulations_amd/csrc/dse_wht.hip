@@ -257,7 +257,7 @@ __device__ __forceinline__ int win_role(int mode, int k, int q) {
 template <int WL, int PASS, int MODE>
 __global__ void __launch_bounds__(WG<WL>::NT)
 k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, const int2* __restrict__ items,
-      int g, int k, int q, int set) {
+      int g, int k, int q, int set, int vsel) {
   __shared__ WhtShared<WL> S;
   const int2 it = items[blockIdx.x];
   const WhtProb& W = probs[it.x];
@@ -294,19 +294,29 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     const int last = has_b<WL>(G.c) ? 1 : 0;
     const LayIdx<WL> is(G, last, tid, xo);
     // both vectors' loads in flight from the start: B's latency hides under A's transposes
+    // (vsel: bit 0 the X-branch vector A, bit 1 the Y-branch vector B -- partitioned registers
+    // transform them in separate launches so one vector's index swap overlaps the other's pass)
     double2 vb[WR];
     gd2* XA = gptr(W.vec_a);
     gd2* XB = gptr(W.vec_b);
+    if (vsel & 1) {
 #pragma unroll
-    for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+      for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+    }
+    if (vsel & 2) {
 #pragma unroll
-    for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
-    tile_fwd<WL>(S.w, v, G.c, tid);
+      for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
+    }
+    if (vsel & 1) {
+      tile_fwd<WL>(S.w, v, G.c, tid);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) gst(XA, is[r], v[r]);
-    tile_fwd<WL>(S.w, vb, G.c, tid);
+      for (int r = 0; r < WR; ++r) gst(XA, is[r], v[r]);
+    }
+    if (vsel & 2) {
+      tile_fwd<WL>(S.w, vb, G.c, tid);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) gst(XB, is[r], vb[r]);
+      for (int r = 0; r < WR; ++r) gst(XB, is[r], vb[r]);
+    }
     return;
   }
 
@@ -317,10 +327,14 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     double2 vb[WR];
     gd2* XA = gptr(W.vec_at);
     gd2* XB = gptr(W.vec_bt);
+    if (vsel & 1) {
 #pragma unroll
-    for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+      for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+    }
+    if (vsel & 2) {
 #pragma unroll
-    for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
+      for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
+    }
     if (tid < 32) {
       const double c = gptr((const double*)W.xytab)[o * 32 + tid];
       if (tid <= WL) S.f[0][tid] = c;
@@ -345,16 +359,20 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
         x[r].y *= d;
       }
     };
-    tile_fwd<WL>(S.w, v, G.c, tid);
-    diag(v, 0);
-    tile_back<WL>(S.w, v, G.c, last, tid);
+    if (vsel & 1) {
+      tile_fwd<WL>(S.w, v, G.c, tid);
+      diag(v, 0);
+      tile_back<WL>(S.w, v, G.c, last, tid);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) gst(XA, ia[r], v[r]);
-    tile_fwd<WL>(S.w, vb, G.c, tid);
-    diag(vb, 1);
-    tile_back<WL>(S.w, vb, G.c, last, tid);
+      for (int r = 0; r < WR; ++r) gst(XA, ia[r], v[r]);
+    }
+    if (vsel & 2) {
+      tile_fwd<WL>(S.w, vb, G.c, tid);
+      diag(vb, 1);
+      tile_back<WL>(S.w, vb, G.c, last, tid);
 #pragma unroll
-    for (int r = 0; r < WR; ++r) gst(XB, ia[r], vb[r]);
+      for (int r = 0; r < WR; ++r) gst(XB, ia[r], vb[r]);
+    }
     return;
   }
 
@@ -519,31 +537,32 @@ __global__ void __launch_bounds__(512) k_wht_qtab(const WhtProb* __restrict__ wp
 
 template <int WL, int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
-                       int g, int k, int q, int set, hipStream_t st) {
+                       int g, int k, int q, int set, int vsel, hipStream_t st) {
   const dim3 grid(n_items), block(WG<WL>::NT);
   if (mode == MODE_APPLY)
-    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_APPLY>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_APPLY>), grid, block, 0, st, wp, dp, items, g, k, q, set, vsel);
   else if (mode == MODE_FIRST)
-    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_FIRST>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_FIRST>), grid, block, 0, st, wp, dp, items, g, k, q, set, vsel);
   else
-    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_GEN>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_GEN>), grid, block, 0, st, wp, dp, items, g, k, q, set, vsel);
   return hipGetLastError();
 }
 
 template <int WL>
 hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const DevProb* dp, const int2* items,
-                    int n_items, int k, int q, int set, hipStream_t st) {
+                    int n_items, int k, int q, int set, int vsel, hipStream_t st) {
   hipError_t e = hipSuccess;
   if (part == WHT_PART_PRE) {
-    e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+    if (vsel & 1) e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
     for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
-      e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, st);
+      e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st);
   } else if (part == WHT_PART_MID) {
-    e = launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, st);
+    e = launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, vsel, st);
   } else {
     for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
-      e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, st);
-    if (e == hipSuccess) e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, st);
+      e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st);
+    if (e == hipSuccess && (vsel & 2))
+      e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
   }
   return e;
 }
@@ -565,11 +584,11 @@ hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64
 }
 
 hipError_t launch_wht_part(int part, int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
-                           const int2* items, int n_items, int k, int q, int set, hipStream_t st) {
+                           const int2* items, int n_items, int k, int q, int set, int vsel, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
-  if (n_groups < 2 || n_groups > kWhtMaxGroups) return hipErrorInvalidValue;
-  if (wl == 12) return wht_part<12>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, st);
-  if (wl == 13) return wht_part<13>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, st);
+  if (n_groups < 2 || n_groups > kWhtMaxGroups || vsel < 1 || vsel > 3) return hipErrorInvalidValue;
+  if (wl == 12) return wht_part<12>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, vsel, st);
+  if (wl == 13) return wht_part<13>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, vsel, st);
   return hipErrorInvalidValue;
 }
 

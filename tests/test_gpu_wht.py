@@ -198,3 +198,26 @@ def test_wht_mixed_context_matches_separate_evolves(engine):
         alone, _ = engine.evolve(t)
         np.testing.assert_allclose(both[i], alone[0], rtol=0, atol=1e-13)
     engine.clear()
+
+
+@pytest.mark.parametrize("n,bits", [(19, 3), (20, 2)])
+def test_wht_swap_overlap_is_schedule_independent(engine, n, bits):
+    """Partitioned registers: the overlapped schedule (each vector's index swap on a second stream
+    under the other vector's pass, option swap_overlap = 1) and the serial one (both swaps between
+    passes) perform the same arithmetic, so their results agree bit for bit."""
+    prob = _random_problem(n, 1900 + n, rare_bit=n - 1)
+    t = np.linspace(0.0, 2e-4, 4)
+    out = {}
+    try:
+        for ov in (0, 1):
+            engine.clear()
+            engine.set_option("swap_overlap", ov)
+            ps = engine.add_sharded(prob, bits)
+            obs, st = engine.evolve(t)
+            assert st["mode"] == 2
+            out[ov] = (obs[ps:ps + (1 << bits)].copy(), engine.state(ps))
+    finally:
+        engine.clear()
+        engine.set_option("swap_overlap", 1)
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--delta", type=float, default=50e3)
     ap.add_argument("--loopback", type=int, default=0, help="all shards on one GPU (2, 4 or 8)")
     ap.add_argument("--wht", type=int, default=1)
+    ap.add_argument("--swap-overlap", type=int, default=1,
+                    help="1: each vector's index swap on a second stream under the other's pass")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                     help="rccl: libdse's RCCL communicator (one GPU per rank); host: the library's host "
                          "exchange backend over torch.distributed gloo (several ranks may share a GPU)")
@@ -51,6 +53,7 @@ def main():
         bits = shard_bits_for(a.loopback)
         with Engine(0) as eng:
             eng.set_option("wht", a.wht)
+            eng.set_option("swap_overlap", a.swap_overlap)
             pid = eng.add_sharded(prob, bits)
             t0 = time.perf_counter()
             obs, st = eng.evolve(np.linspace(0.0, a.t_final, a.steps))
@@ -66,6 +69,7 @@ def main():
         dist.init_process_group("gloo")       # bootstrap (rccl) or the data path itself (host)
         with Engine(dev) as eng:
             eng.set_option("wht", a.wht)
+            eng.set_option("swap_overlap", a.swap_overlap)
             if a.transport == "rccl":
                 join(eng, rank, world, dist)
             else:
@@ -109,6 +113,7 @@ def main():
             "wall_s": wall, "h_applications": st["h_applications"],
             "ms_per_h_application": wall / max(st["h_applications"], 1) * 1e3,
             "shard_GiB": shard_bytes / 2**30, "engine_mode": st.get("mode"),
+            "swap_overlap": a.swap_overlap,
             "exchange": "index-swap all-to-all of A, B (x2)" if wht else f"send/recv, {n_masks} partner masks",
             "exchange_bytes_per_h_per_rank": xbytes,
             "exchange_bytes_measured_per_rank": measured,
