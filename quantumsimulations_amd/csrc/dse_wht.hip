@@ -254,10 +254,10 @@ __device__ __forceinline__ int win_role(int mode, int k, int q) {
   return ((k - 1) & 1) ? 1 : (q ? 2 : 0);
 }
 
-template <int WL, int PASS, int MODE>
+template <int WL, int PASS, int MODE, int VSEL>
 __global__ void __launch_bounds__(WG<WL>::NT)
 k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, const int2* __restrict__ items,
-      int g, int k, int q, int set, int vsel) {
+      int g, int k, int q, int set) {
   __shared__ WhtShared<WL> S;
   const int2 it = items[blockIdx.x];
   const WhtProb& W = probs[it.x];
@@ -294,25 +294,26 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     const int last = has_b<WL>(G.c) ? 1 : 0;
     const LayIdx<WL> is(G, last, tid, xo);
     // both vectors' loads in flight from the start: B's latency hides under A's transposes
-    // (vsel: bit 0 the X-branch vector A, bit 1 the Y-branch vector B -- partitioned registers
-    // transform them in separate launches so one vector's index swap overlaps the other's pass)
+    // (VSEL: bit 0 the X-branch vector A, bit 1 the Y-branch vector B -- partitioned registers
+    // transform them in separate launches so one vector's index swap overlaps the other's pass;
+    // compile-time, so the tile arrays stay in registers)
     double2 vb[WR];
     gd2* XA = gptr(W.vec_a);
     gd2* XB = gptr(W.vec_b);
-    if (vsel & 1) {
+    if constexpr ((VSEL & 1) != 0) {
 #pragma unroll
       for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
     }
-    if (vsel & 2) {
+    if constexpr ((VSEL & 2) != 0) {
 #pragma unroll
       for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
     }
-    if (vsel & 1) {
+    if constexpr ((VSEL & 1) != 0) {
       tile_fwd<WL>(S.w, v, G.c, tid);
 #pragma unroll
       for (int r = 0; r < WR; ++r) gst(XA, is[r], v[r]);
     }
-    if (vsel & 2) {
+    if constexpr ((VSEL & 2) != 0) {
       tile_fwd<WL>(S.w, vb, G.c, tid);
 #pragma unroll
       for (int r = 0; r < WR; ++r) gst(XB, is[r], vb[r]);
@@ -327,11 +328,11 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     double2 vb[WR];
     gd2* XA = gptr(W.vec_at);
     gd2* XB = gptr(W.vec_bt);
-    if (vsel & 1) {
+    if constexpr ((VSEL & 1) != 0) {
 #pragma unroll
       for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
     }
-    if (vsel & 2) {
+    if constexpr ((VSEL & 2) != 0) {
 #pragma unroll
       for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
     }
@@ -359,14 +360,14 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
         x[r].y *= d;
       }
     };
-    if (vsel & 1) {
+    if constexpr ((VSEL & 1) != 0) {
       tile_fwd<WL>(S.w, v, G.c, tid);
       diag(v, 0);
       tile_back<WL>(S.w, v, G.c, last, tid);
 #pragma unroll
       for (int r = 0; r < WR; ++r) gst(XA, ia[r], v[r]);
     }
-    if (vsel & 2) {
+    if constexpr ((VSEL & 2) != 0) {
       tile_fwd<WL>(S.w, vb, G.c, tid);
       diag(vb, 1);
       tile_back<WL>(S.w, vb, G.c, last, tid);
@@ -535,17 +536,30 @@ __global__ void __launch_bounds__(512) k_wht_qtab(const WhtProb* __restrict__ wp
   }
 }
 
+template <int WL, int PASS, int VSEL>
+hipError_t launch_pass_v(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
+                         int g, int k, int q, int set, hipStream_t st) {
+  const dim3 grid(n_items), block(WG<WL>::NT);
+  if (mode == MODE_APPLY)
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_APPLY, VSEL>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+  else if (mode == MODE_FIRST)
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_FIRST, VSEL>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+  else
+    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_GEN, VSEL>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+  return hipGetLastError();
+}
+
+// FIRST and FINAL always take both vectors; FWD / MID / INV one (vsel 1, 2) or both (3)
 template <int WL, int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
                        int g, int k, int q, int set, int vsel, hipStream_t st) {
-  const dim3 grid(n_items), block(WG<WL>::NT);
-  if (mode == MODE_APPLY)
-    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_APPLY>), grid, block, 0, st, wp, dp, items, g, k, q, set, vsel);
-  else if (mode == MODE_FIRST)
-    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_FIRST>), grid, block, 0, st, wp, dp, items, g, k, q, set, vsel);
-  else
-    hipLaunchKernelGGL((k_wht<WL, PASS, MODE_GEN>), grid, block, 0, st, wp, dp, items, g, k, q, set, vsel);
-  return hipGetLastError();
+  if constexpr (PASS == WHT_FIRST || PASS == WHT_FINAL) {
+    return launch_pass_v<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
+  } else {
+    if (vsel == 3) return launch_pass_v<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
+    if (vsel == 1) return launch_pass_v<WL, PASS, 1>(mode, wp, dp, items, n_items, g, k, q, set, st);
+    return launch_pass_v<WL, PASS, 2>(mode, wp, dp, items, n_items, g, k, q, set, st);
+  }
 }
 
 template <int WL>
