@@ -104,3 +104,31 @@ def test_production_path_is_repeatable_in_one_context(engine, m):
         engine.clear()
     for r in runs[1:]:
         assert np.array_equal(r, runs[0])
+
+
+def test_reference_grid_intervals_match_fine_stepping_n14(engine):
+    """The full-sweep regime of config 3: the reference's own grid (t_final 30 s, 20000 outputs,
+    sweep_sea_detuning.py:1223-1224) puts ~1e4 Chebyshev terms into one interval (alpha dt ~ 1e4,
+    one output per launch).  Its first two intervals, on the production interval kernel for all
+    three variants at delta 0 and 150 kHz, against the same evolutions stepped through 150
+    sub-intervals each (10 us, two outputs per launch, ~100 terms per launch): the propagator is
+    exact at both degrees, so the observables agree to 1e-10 and the norm stays 1 to 1e-12."""
+    t_ref = np.linspace(0.0, 30.0, 20000)[:3]
+    t_fine = np.concatenate([np.linspace(t_ref[0], t_ref[1], 151), np.linspace(t_ref[1], t_ref[2], 151)[1:]])
+    assert t_fine[150] == t_ref[1] and t_fine[300] == t_ref[2]
+    probs = [pb.build_problem(sweep_point_params(13, float(d), v, 30.0, 20000))
+             for v in VARIANTS for d in (0.0, 150e3)]
+    engine.clear()
+    try:
+        for p in probs:
+            engine.add(p)
+        coarse, st_c = engine.evolve(t_ref)
+        fine, st_f = engine.evolve(t_fine)
+    finally:
+        engine.clear()
+    assert st_c["mode"] == 1 and st_c["outputs_per_launch"] == 1 and st_c["max_degree"] > 5000
+    assert st_f["mode"] == 1 and st_f["max_degree"] < 1000
+    worst = float(np.max(np.abs(coarse[:, :6, :] - fine[:, :6, ::150])))
+    assert worst < 1e-10, worst
+    np.testing.assert_allclose(coarse[:, 6, :], 1.0, rtol=0, atol=1e-12)
+    print(f"N=14 reference grid: degree {st_c['max_degree']} vs stepped, max |d<O>| = {worst:.2e}")
