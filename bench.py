@@ -68,6 +68,8 @@ def parse():
                     "the persistent interval kernel")
     ap.add_argument("--outputs-per-launch", type=int, default=int(os.environ.get("DSE_OUTPUTS_PER_LAUNCH", "2")),
                     help="persistent mode: output times propagated per launch from one Chebyshev series")
+    ap.add_argument("--mixed-launch", type=int, default=int(os.environ.get("DSE_MIXED_LAUNCH", "0")),
+                    help="persistent mode: 1- and 2-tile problems in one launch per interval (1)")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
     ap.add_argument("--n-det", type=int, default=N_DET)
     ap.add_argument("--no-large", action="store_true", help="skip the config-5 single-GPU leg")
@@ -340,6 +342,7 @@ def main():
     eng.set_option("streams", args.streams)
     eng.set_option("persistent", 0 if args.streaming else 1)
     eng.set_option("outputs_per_launch", args.outputs_per_launch)
+    eng.set_option("mixed_launch", args.mixed_launch)
     if os.environ.get("DSE_CORESIDENT"):  # diagnostics: workgroups per 2-tile interval launch chunk
         eng.set_option("coresident", float(os.environ["DSE_CORESIDENT"]))
     for p in probs:

@@ -137,6 +137,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
  *          "max_degree"   Chebyshev degree cap per interval (default 2e6)
+ *          "mixed_launch" persistent mode: 1 puts the 1- and 2-tile problems of one tile size in
+ *                         one interval launch (stiffest pairs, 1-tile problems, remaining pairs)
+ *                         when all 2-tile workgroups fit at once; 0 (default) one stream each
  *          "handoff_fences"  persistent mode, 2-tile registers: 0 (default) the sc1 hand-off
  *                         (write-through payload, per-wave vmcnt(0) + barrier, sc1 flag and
  *                         poll); 1 adds an agent-scope release before every flag store and an

@@ -123,6 +123,7 @@ struct dse_ctx {
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
+  int mixed_launch = 0;             // persistent: 1- and 2-tile problems of one tile size in one launch
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
   int handoff_fallbacks = 0;        // evolves re-run on the streaming kernels after a hand-off timeout
@@ -1062,6 +1063,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     HIPC(set_spin_limit((int)value));
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
+  } else if (k == "mixed_launch") {
+    ctx->mixed_launch = value != 0.0;
   } else if (k == "time_kernels") {
     if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
     ctx->time_every = (int)value;
@@ -1794,6 +1797,38 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   int n_big = 0;
   for (auto& P : ctx->probs) n_big += P.sm ? 0 : 1;
   const int n_lanes = any_dist ? 1 : std::max(1, std::min<int>(ctx->n_streams, n_big));
+  bool imag_all = true;
+  for (auto& P : ctx->probs) imag_all = imag_all && (P.sm || P.imag);
+  // 2-tile interval launches go out in chunks whose workgroups can all be resident at once (the
+  // pairs hand off every term): the occupancy query x compute units, even.
+  int64_t pair_cap = 2;
+  if (persistent) {
+    int per_cu = 1;
+    if (ctx->coresident > 0) {
+      pair_cap = ctx->coresident;
+    } else {
+      HIPC(interval_occupancy(13, imag_all, &per_cu));
+      pair_cap = (int64_t)std::max(1, per_cu) * ctx->n_cu;
+    }
+    pair_cap = std::max<int64_t>(2, pair_cap / 2 * 2);
+  }
+  const int64_t cap = pair_cap;
+  // Mixed launches (option mixed_launch): the 1- and 2-tile problems of one tile size share one
+  // launch per interval instead of one stream each, so the 1-tile problems run in the CUs the
+  // light 2-tile problems leave, inside the launch, and never hold a CU the next launch's stiff
+  // pairs need.  Only when every 2-tile workgroup fits at once (2P <= cap): the 1-tile problems
+  // and the lightest pairs beyond the first cap workgroups are dispatched as CUs free up, and a
+  // pair whose partner is still queued waits only for a workgroup that needs no partner.
+  std::map<int, std::pair<int64_t, int64_t>> tiles_per_L;  // L -> (1-tile problems, 2-tile problems)
+  for (auto& P : ctx->probs)
+    if (!P.sm && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
+      (P.n_tiles == 1 ? tiles_per_L[P.L].first : tiles_per_L[P.L].second) += 1;
+  auto mixed_L = [&](const HostProblem& P) {
+    if (!persistent || !ctx->mixed_launch || P.sm || P.shard_bits != 0 || P.n_tiles > 2) return false;
+    const auto it = tiles_per_L.find(P.L);
+    return it != tiles_per_L.end() && it->second.first > 0 && it->second.second > 0 &&
+           2 * it->second.second <= cap;
+  };
   std::vector<int> order;
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
     if (!ctx->probs[pi].sm) order.push_back((int)pi);
@@ -1804,9 +1839,10 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   std::vector<std::map<std::pair<int, int64_t>, std::vector<int>>> lane_probs(n_lanes);
   for (size_t i = 0; i < order.size(); ++i) {
     const HostProblem& P = ctx->probs[order[i]];
-    const std::pair<int, int64_t> key(P.L, P.n_tiles);
+    const bool mixed = mixed_L(P);
+    const std::pair<int, int64_t> key(P.L, mixed ? 0 : P.n_tiles);  // tiles 0: a mixed group
     int lane = (int)(i % n_lanes);
-    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1) ? 0 : 1;
+    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1 || mixed) ? 0 : 1;
     // shards of one register read each other's vectors: same lane, hence the same launches
     if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);
@@ -1868,22 +1904,6 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     max_deg = std::max(max_deg, ln.max_deg);
   }
   HIPC(hipMemcpy(ctx->d_items, items.data(), items.size() * sizeof(int2), hipMemcpyHostToDevice));
-  bool imag_all = true;
-  for (auto& P : ctx->probs) imag_all = imag_all && (P.sm || P.imag);
-  // 2-tile interval launches go out in chunks whose workgroups can all be resident at once (the
-  // pairs hand off every term): the occupancy query x compute units, even.
-  int64_t pair_cap = 2;
-  if (persistent) {
-    int per_cu = 1;
-    if (ctx->coresident > 0) {
-      pair_cap = ctx->coresident;
-    } else {
-      HIPC(interval_occupancy(13, imag_all, &per_cu));
-      pair_cap = (int64_t)std::max(1, per_cu) * ctx->n_cu;
-    }
-    pair_cap = std::max<int64_t>(2, pair_cap / 2 * 2);
-  }
-  const int64_t cap = pair_cap;
   if (persistent) {
     // Interval-kernel order of 2-tile groups: the two tiles of a problem exchange data every
     // term, so place them 8 blocks apart -- blocks b and b + 8 land on one XCD under the
@@ -1892,6 +1912,37 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     std::vector<int2> iv = items;
     for (auto& ln : ctx->lanes)
       for (auto& g : ln.groups) {
+        if (g.tiles == 0) {
+          // mixed group: the stiffest pairs first (as many as fit beside the 1-tile problems), then
+          // the 1-tile problems, then the remaining pairs, each segment in degree order; pairs in
+          // blocks of 16 with their tiles 8 apart, as below
+          std::vector<int2> pr, sg;
+          for (int64_t i = 0; i < g.count; ++i) {
+            const int2 e = items[g.off + i];
+            (ctx->probs[e.x].n_tiles == 2 ? pr : sg).push_back(e);
+          }
+          const int64_t np = (int64_t)pr.size() / 2, ns = (int64_t)sg.size();
+          const int64_t h = std::min<int64_t>(np, std::max<int64_t>(0, (cap - ns) / 2));
+          int64_t o = g.off;
+          auto put_pairs = [&](int64_t p0, int64_t p1) {
+            for (int64_t b0 = p0; b0 < p1; b0 += 8) {
+              const int64_t m = std::min<int64_t>(8, p1 - b0);
+              if (ctx->xcd_pairs) {
+                for (int64_t i = 0; i < m; ++i) {
+                  iv[o + i] = pr[2 * (b0 + i)];
+                  iv[o + m + i] = pr[2 * (b0 + i) + 1];
+                }
+              } else {
+                for (int64_t i = 0; i < 2 * m; ++i) iv[o + i] = pr[2 * b0 + i];
+              }
+              o += 2 * m;
+            }
+          };
+          put_pairs(0, h);
+          for (const int2& e : sg) iv[o++] = e;
+          put_pairs(h, np);
+          continue;
+        }
         if (g.tiles != 2 || !ctx->xcd_pairs) continue;
         for (int64_t off = 0; off < g.count; off += cap) {
           const int64_t cnt = std::min<int64_t>(cap, g.count - off);
@@ -2024,8 +2075,8 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
         const int T = 1 << g.L;
         if (persistent) {
           // all K terms of the interval in one launch; 2-tile groups in co-resident chunks
-          if (g.tiles == 2) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
-          const int64_t gcap = g.tiles == 2 ? cap : g.count;
+          if (g.tiles != 1) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
+          const int64_t gcap = g.tiles == 2 ? cap : g.count;  // mixed (0): one launch, see above
           for (int64_t off = 0; off < g.count; off += gcap) {
             const int cnt = (int)std::min<int64_t>(gcap, g.count - off);
             double fl = 0.0, am = 0.0;

@@ -132,3 +132,28 @@ def test_reference_grid_intervals_match_fine_stepping_n14(engine):
     assert worst < 1e-10, worst
     np.testing.assert_allclose(coarse[:, 6, :], 1.0, rtol=0, atol=1e-12)
     print(f"N=14 reference grid: degree {st_c['max_degree']} vs stepped, max |d<O>| = {worst:.2e}")
+
+
+def test_mixed_launch_is_bitwise_identical(engine):
+    """Option mixed_launch: the 1- and 2-tile problems of the config-3 points in one interval launch
+    (stiffest pairs, then the 1-tile problems, then the remaining pairs) instead of one stream
+    each.  Only the dispatch order changes, so every problem's results are bitwise those of the
+    default two-stream schedule, and the run stays on the persistent kernel."""
+    t = np.linspace(0.0, 2e-4, 21)
+    res = {}
+    for mixed in (0, 1, 1):
+        engine.clear()
+        engine.set_option("mixed_launch", mixed)
+        try:
+            for variant in VARIANTS:
+                for delta in DELTAS:
+                    engine.add(pb.build_problem(_params(variant, delta, t)))
+            obs, st = engine.evolve(t)
+        finally:
+            engine.set_option("mixed_launch", 0)
+            engine.clear()
+        assert st["mode"] == 1
+        if mixed in res:
+            assert np.array_equal(obs, res[mixed])
+        res[mixed] = obs
+    assert np.array_equal(res[1], res[0])
