@@ -189,6 +189,31 @@ def _contrast_figure(plt, rows):
     return f
 
 
+def write_point_pngs(details, dpi: int = 300) -> int:
+    """The per-point PNGs of ``details`` ((det_dir, per, metrics, det) rows of write_sweep) only:
+    a unit of work a worker process can take on its own (PNG reports have no page order)."""
+    plt = _plt()
+    n = 0
+    for det_dir, per, metrics, det in details:
+        for name, f in point_figures(per, metrics, det):
+            f.savefig(os.path.join(det_dir, name), dpi=dpi)
+            plt.close(f)
+            n += 1
+    return n
+
+
+def write_contrast_png(base_dir: str, rows: List[dict], dpi: int = 300) -> None:
+    """The sweep-level contrast plot of a PNG report (as write_sweep_report writes it)."""
+    plt = _plt()
+    try:
+        f = _contrast_figure(plt, rows)
+        if f is not None:
+            f.savefig(os.path.join(base_dir, "contrast_rare_center_vs_DeltaOmega_over_geff.png"), dpi=dpi)
+            plt.close(f)
+    except Exception as exc:  # the reference only warns here (:1149-1150)
+        print(f"Warning: could not build ΔΩ/|g_eff| contrast plot: {exc}")
+
+
 def write_sweep_report(base_dir: str, global_params: dict, rows: List[dict], details,
                        pdf: bool = True, dpi: int = 300) -> None:
     """PNGs of every point (+ the contrast plot) and, with ``pdf``, sea_detuning_report.pdf."""

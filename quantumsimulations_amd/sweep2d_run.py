@@ -9,9 +9,11 @@ The reference produces this data by running ``sweep_sea_detuning.py`` once per f
 * every sweep is planned first (directory, geometry, parameter records: ``sweep_runner.plan_sweep``);
 * the evolutions of a group of sweeps go to ``evolve_many`` together (spread over all GPUs,
   longest-first), so each GPU holds a full batch even when one sweep alone would not fill it;
-* the per-point files, metrics and figures of a finished group are written by a worker process
-  while the next group's evolutions run on the GPUs (report generation off
-  the critical path);
+* the per-point files, metrics and figures of a finished group are written by worker processes
+  (this process's CPU share less one, at most 16) while the next group's evolutions run on the
+  GPUs (report generation off the critical path); PNG reports go out as
+  one task per sweep tree and then one per 4 points, so the figure drawing (most of the host
+  work) spreads over every worker rather than one per sweep;
 * finally the headless 2D report (``sweep2d``) runs over the root: contrast summary PDF/PNGs and,
   with ``--stable``, the stable-region JSON.
 
@@ -38,10 +40,34 @@ from .sweep import GAMMA_RARE, GAMMA_SEA, PHI, SWEEP_TOL, f_az_hz
 from .sweep_runner import SweepPlan, evolve_many, plan_sweep, write_sweep
 
 
-def _write(plan: SweepPlan, traces, report: str) -> Dict[str, float]:
+def _write(plan: SweepPlan, traces, report: str, keep_details: bool = False):
+    """A sweep's files, metrics and summary (and its report unless the PNGs are split off):
+    timings, plus the rows the PNG tasks draw from when ``keep_details``."""
     timings: Dict[str, float] = {}
-    write_sweep(plan, traces, report=report, timings=timings, verbose=False)
-    return timings
+    details: list = []
+    write_sweep(plan, traces, report=report, timings=timings, verbose=False,
+                details_out=details if keep_details else None)
+    return timings, details
+
+
+def _pngs(details, base_dir: Optional[str] = None, rows=None) -> Dict[str, float]:
+    """One PNG task: the figures of a chunk of points (and the sweep's contrast plot, once)."""
+    from . import report as rep
+    t0 = time.perf_counter()
+    rep.write_point_pngs(details)
+    if base_dir is not None:
+        rep.write_contrast_png(base_dir, rows)
+    return {"report_s": time.perf_counter() - t0}
+
+
+def writer_count() -> int:
+    """Worker processes for the sweep trees and reports: this process's CPU share less the one
+    driving the GPUs, at most 16 (the GPU box's share; os.cpu_count() there is the machine's)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        n = os.cpu_count() or 2
+    return max(1, min(16, n - 1))
 
 
 def run_2d_sweep(root: str, f1a_hz: Sequence[float], n_det: int = 64, n_sea: int = 13,
@@ -67,9 +93,31 @@ def run_2d_sweep(root: str, f1a_hz: Sequence[float], n_det: int = 64, n_sea: int
         devices = list(range(device_count()))
     if group <= 0:  # enough sweeps per evolve call for ~64 evolutions (a full batch) per GPU
         group = max(1, int(np.ceil(64 * max(len(devices), 1) / (3 * n_det))))
-    evolve_s, futures = 0.0, []
+    evolve_s, futures, tree_futs = 0.0, [], []
+    # PNG reports are split per point: the sweep's files first (one task), then its figures in
+    # chunks of points over all workers, submitted as each tree task finishes -- figure drawing
+    # is most of the host work (~0.5 s per point at 300 dpi), and one task per sweep left it to
+    # at most as many workers as sweeps.  PDF reports keep one task per sweep (page order).
+    split = report == "png"
+    n_workers = writer_count()
+    chunk = 4
+
+    def submit_pngs(pool, block: bool) -> None:
+        for f in list(tree_futs):
+            if not (block or f.done()):
+                continue
+            tree_futs.remove(f)
+            timings, details = f.result()
+            futures.append(timings)
+            if not details:
+                continue
+            base, rows = os.path.dirname(details[0][0]), [d[2] for d in details]
+            for i in range(0, len(details), chunk):
+                futures.append(pool.submit(_pngs, details[i:i + chunk], base if i == 0 else None,
+                                           rows if i == 0 else None))
+
     ctx = mp.get_context("spawn")  # the writer never inherits this process's GPU contexts
-    with ProcessPoolExecutor(max_workers=min(4, len(plans)), mp_context=ctx) as pool:
+    with ProcessPoolExecutor(max_workers=n_workers, mp_context=ctx) as pool:
         for g0 in range(0, len(plans), group):
             grp = plans[g0:g0 + group]
             flat = [p for plan in grp for p in plan.flat]
@@ -81,10 +129,16 @@ def run_2d_sweep(root: str, f1a_hz: Sequence[float], n_det: int = 64, n_sea: int
             off = 0
             for plan in grp:
                 n = len(plan.flat)
-                futures.append(pool.submit(_write, plan, traces[off:off + n], report))
+                if split:
+                    tree_futs.append(pool.submit(_write, plan, traces[off:off + n], "none", True))
+                else:
+                    futures.append(pool.submit(_write, plan, traces[off:off + n], report))
                 off += n
+            submit_pngs(pool, block=False)
         t_wait = time.perf_counter()
-        writer = [f.result() for f in futures]
+        submit_pngs(pool, block=True)
+        writer = [f if isinstance(f, dict) else f.result() for f in futures]
+        writer = [w[0] if isinstance(w, tuple) else w for w in writer]
     t_written = time.perf_counter()
     pdf = os.path.join(root, "contrast_vs_coupling_summary.pdf")
     if stable:
@@ -95,7 +149,7 @@ def run_2d_sweep(root: str, f1a_hz: Sequence[float], n_det: int = 64, n_sea: int
     t_end = time.perf_counter()
     out = {"root": root, "sweep_dirs": [p.base_dir for p in plans],
            "evolutions": sum(len(p.flat) for p in plans), "devices": list(devices),
-           "group": group, "evolve_s": evolve_s,
+           "group": group, "writers": n_workers, "evolve_s": evolve_s,
            "writer_s_total": sum(w.get("outputs_s", 0.0) + w.get("report_s", 0.0) for w in writer),
            "writer_tail_s": t_written - t_wait, "report2d_s": t_end - t_written,
            "wall_s": t_end - t_start}

@@ -250,9 +250,11 @@ def plan_sweep(
 
 
 def write_sweep(plan: SweepPlan, traces: Sequence[Trace], report: str = "full",
-                timings: Optional[Dict[str, float]] = None, verbose: bool = True) -> str:
+                timings: Optional[Dict[str, float]] = None, verbose: bool = True,
+                details_out: Optional[list] = None) -> str:
     """Per-point files and metrics in detuning order, the report, global_params.json and
-    summary.json (:611-1157) from the evolutions' traces (in ``plan.flat`` order)."""
+    summary.json (:611-1157) from the evolutions' traces (in ``plan.flat`` order).
+    ``details_out``: receives the (det_dir, per, metrics, det) rows a report is drawn from."""
     if report not in ("full", "png", "none"):
         raise ValueError(f"report must be 'full', 'png' or 'none', not {report!r}")
     say = print if verbose else (lambda *a, **k: None)
@@ -278,6 +280,8 @@ def write_sweep(plan: SweepPlan, traces: Sequence[Trace], report: str = "full",
         summary["sweep_results"].append(metrics)
         details.append((det_dir, per, metrics, det))
     t2 = time.perf_counter()
+    if details_out is not None:
+        details_out.extend(details)
 
     if report != "none":
         from . import report as rep

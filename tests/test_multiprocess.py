@@ -197,3 +197,34 @@ def test_config4_driver_pipeline_with_fake_engine(monkeypatch, tmp_path):
         s = json.load(open(os.path.join(d, "summary.json")))
         assert s["global_params"]["f1A_Hz"] == f1a and len(s["sweep_results"]) == 4
     assert os.path.exists(os.path.join(str(tmp_path), "contrast_vs_coupling_summary.pdf"))
+
+
+def test_config4_driver_png_reports_split_over_workers(monkeypatch, tmp_path):
+    """sweep2d_run with PNG reports: each sweep tree is written by one task, then its figures in
+    per-point chunks over the worker pool -- every point directory gets the reference's PNGs and
+    each sweep its contrast plot, as in the one-task-per-sweep form."""
+    import glob
+    import os
+    from quantumsimulations_amd import engine as eng_mod
+    from quantumsimulations_amd.sweep2d_run import run_2d_sweep, writer_count
+
+    class Sloped(_FakeEngine):
+        def evolve(self, t, tol=1e-14):
+            obs, st = super().evolve(t, tol)
+            for i, p in enumerate(self.probs):
+                tt = np.asarray(t) * 1e3
+                obs[i, 2] = -1.0 + (1.0 + 0.37 * p.n_qubits + 1e-6 * p.shift) * tt + 0.01 * np.sin(41.0 * tt)
+            return obs, st
+    monkeypatch.setattr(eng_mod, "Engine", Sloped)
+    monkeypatch.setattr(eng_mod, "device_memory", lambda dev: (64e9, 288e9))
+    _FakeEngine.log = []
+    out = run_2d_sweep(str(tmp_path), [5e3, 20e3], n_det=4, n_sea=5, t_final=1e-4, steps=11,
+                       coarse_window=2, devices=[0], report="png", group=1, verbose=False)
+    assert out["writers"] == writer_count() >= 1
+    for d in out["sweep_dirs"]:
+        points = [p for p in glob.glob(os.path.join(d, "delta_*")) if os.path.isdir(p)]
+        assert len(points) == 4
+        for p in points:
+            assert len(glob.glob(os.path.join(p, "*.png"))) >= 2, p
+        assert os.path.exists(os.path.join(d, "contrast_rare_center_vs_DeltaOmega_over_geff.png"))
+        assert os.path.exists(os.path.join(d, "summary.json"))
