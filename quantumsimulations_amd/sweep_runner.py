@@ -66,6 +66,38 @@ def assign_lpt(costs: Sequence[float], n_bins: int) -> List[List[int]]:
     return bins
 
 
+# One libdse context per (engine class, device), kept across evolve_many calls of this process: a
+# driver that evolves sweep after sweep (sweep2d_run: one call per group of f1A sweeps) pays the
+# context set-up and the first call's allocations once instead of per call (~0.1-0.2 s each).
+# DSE_ENGINE_CACHE=0 opens and closes a context per call, as before.
+_ENGINES: Dict[Tuple[type, int], Any] = {}
+_ENGINES_LOCK = threading.Lock()
+
+
+def _engine_for(cls, dev: int):
+    if os.environ.get("DSE_ENGINE_CACHE", "1") == "0":
+        return cls(dev), True
+    with _ENGINES_LOCK:
+        eng = _ENGINES.get((cls, dev))
+        if eng is None:
+            eng = _ENGINES[(cls, dev)] = cls(dev)
+    return eng, False
+
+
+def close_engines() -> None:
+    """Closes the contexts evolve_many keeps (also at interpreter exit)."""
+    with _ENGINES_LOCK:
+        for eng in _ENGINES.values():
+            close = getattr(eng, "close", None)
+            if close is not None:
+                close()
+        _ENGINES.clear()
+
+
+import atexit as _atexit  # noqa: E402
+_atexit.register(close_engines)
+
+
 def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequence[int]] = None,
                 tol: Optional[float] = None) -> List[Trace]:
     """``simulate_rare`` for every parameter set, spread over ``devices`` (one host thread and one
@@ -88,26 +120,36 @@ def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequ
 
     def work(dev: int, idxs: List[int]) -> None:
         from .engine import Engine, batches_for_memory, evolve_groups
+        eng, own = None, False
         try:
-            with Engine(dev) as eng:
-                # one evolve per time grid and engine class, within the device's memory
-                sub = evolve_groups([(float(params_list[i].t_final), int(params_list[i].steps))
-                                     for i in idxs], [probs[i] for i in idxs])
-                for local in sub.values():
-                    group = [idxs[j] for j in local]
+            eng, own = _engine_for(Engine, dev)
+            # one evolve per time grid and engine class, within the device's memory
+            sub = evolve_groups([(float(params_list[i].t_final), int(params_list[i].steps))
+                                 for i in idxs], [probs[i] for i in idxs])
+            for local in sub.values():
+                group = [idxs[j] for j in local]
+                eng.clear()
+                for batch in batches_for_memory([probs[i] for i in group], dev):
                     eng.clear()
-                    for batch in batches_for_memory([probs[i] for i in group], dev):
-                        eng.clear()
-                        members = [group[b] for b in batch]
-                        for i in members:
-                            eng.add(probs[i])
-                        t = grids[members[0]]
-                        obs, _ = eng.evolve(t, tol=tol)
-                        for slot, i in enumerate(members):
-                            results[i] = (t.copy(), {name: obs[slot, j].copy()
-                                                     for j, name in enumerate(OBS_NAMES)})
+                    members = [group[b] for b in batch]
+                    for i in members:
+                        eng.add(probs[i])
+                    t = grids[members[0]]
+                    obs, _ = eng.evolve(t, tol=tol)
+                    for slot, i in enumerate(members):
+                        results[i] = (t.copy(), {name: obs[slot, j].copy()
+                                                 for j, name in enumerate(OBS_NAMES)})
+            eng.clear()
         except BaseException as exc:  # re-raised in the caller's thread
             errors.append(exc)
+            if eng is not None and not own:  # a failed context is not reused
+                with _ENGINES_LOCK:
+                    if _ENGINES.get((Engine, dev)) is eng:
+                        del _ENGINES[(Engine, dev)]
+                        own = True
+        finally:
+            if eng is not None and own and hasattr(eng, "close"):
+                eng.close()
 
     threads = [threading.Thread(target=work, args=(d, s)) for d, s in zip(devices, shares) if s]
     for th in threads:
