@@ -215,8 +215,9 @@ def write_contrast_png(base_dir: str, rows: List[dict], dpi: int = 300) -> None:
 
 
 def write_sweep_report(base_dir: str, global_params: dict, rows: List[dict], details,
-                       pdf: bool = True, dpi: int = 300) -> None:
-    """PNGs of every point (+ the contrast plot) and, with ``pdf``, sea_detuning_report.pdf."""
+                       pdf: bool = True, dpi: int = 300, pngs: bool = True) -> None:
+    """PNGs of every point (+ the contrast plot) and, with ``pdf``, sea_detuning_report.pdf;
+    ``pngs=False``: the PDF alone (the PNGs drawn elsewhere, e.g. by worker processes)."""
     plt = _plt()
     from matplotlib.backends.backend_pdf import PdfPages
     pages = PdfPages(os.path.join(base_dir, "sea_detuning_report.pdf")) if pdf else None
@@ -226,8 +227,11 @@ def write_sweep_report(base_dir: str, global_params: dict, rows: List[dict], det
             pages.savefig(f)
             plt.close(f)
         for det_dir, per, metrics, det in details:
+            if not pngs and pages is None:
+                break
             for name, f in point_figures(per, metrics, det):
-                f.savefig(os.path.join(det_dir, name), dpi=dpi)
+                if pngs:
+                    f.savefig(os.path.join(det_dir, name), dpi=dpi)
                 if pages is not None:
                     pages.savefig(f)
                 plt.close(f)
@@ -238,8 +242,9 @@ def write_sweep_report(base_dir: str, global_params: dict, rows: List[dict], det
         try:
             f = _contrast_figure(plt, rows)
             if f is not None:
-                f.savefig(os.path.join(base_dir, "contrast_rare_center_vs_DeltaOmega_over_geff.png"),
-                          dpi=dpi)
+                if pngs:
+                    f.savefig(os.path.join(base_dir, "contrast_rare_center_vs_DeltaOmega_over_geff.png"),
+                              dpi=dpi)
                 if pages is not None:
                     pages.savefig(f)
                 plt.close(f)

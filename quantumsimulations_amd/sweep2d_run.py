@@ -37,7 +37,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from .sweep import GAMMA_RARE, GAMMA_SEA, PHI, SWEEP_TOL, f_az_hz
-from .sweep_runner import SweepPlan, evolve_many, plan_sweep, write_sweep
+from .sweep_runner import SweepPlan, _png_chunk, evolve_many, plan_sweep, write_sweep, writer_count
 
 
 def _write(plan: SweepPlan, traces, report: str, keep_details: bool = False):
@@ -46,28 +46,13 @@ def _write(plan: SweepPlan, traces, report: str, keep_details: bool = False):
     timings: Dict[str, float] = {}
     details: list = []
     write_sweep(plan, traces, report=report, timings=timings, verbose=False,
-                details_out=details if keep_details else None)
+                details_out=details if keep_details else None, workers=1)
     return timings, details
 
 
 def _pngs(details, base_dir: Optional[str] = None, rows=None) -> Dict[str, float]:
     """One PNG task: the figures of a chunk of points (and the sweep's contrast plot, once)."""
-    from . import report as rep
-    t0 = time.perf_counter()
-    rep.write_point_pngs(details)
-    if base_dir is not None:
-        rep.write_contrast_png(base_dir, rows)
-    return {"report_s": time.perf_counter() - t0}
-
-
-def writer_count() -> int:
-    """Worker processes for the sweep trees and reports: this process's CPU share less the one
-    driving the GPUs, at most 16 (the GPU box's share; os.cpu_count() there is the machine's)."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover - non-Linux
-        n = os.cpu_count() or 2
-    return max(1, min(16, n - 1))
+    return {"report_s": _png_chunk(details, base_dir, rows)}
 
 
 def run_2d_sweep(root: str, f1a_hz: Sequence[float], n_det: int = 64, n_sea: int = 13,

@@ -228,3 +228,41 @@ def test_config4_driver_png_reports_split_over_workers(monkeypatch, tmp_path):
             assert len(glob.glob(os.path.join(p, "*.png"))) >= 2, p
         assert os.path.exists(os.path.join(d, "contrast_rare_center_vs_DeltaOmega_over_geff.png"))
         assert os.path.exists(os.path.join(d, "summary.json"))
+
+
+def test_write_sweep_png_workers_match_serial_report(tmp_path):
+    """write_sweep with worker processes for the per-point PNGs (8 points, 4-point chunks) writes
+    the same files as the serial report, and the PDF the same pages (drawn in this process)."""
+    import os
+    import re
+    from quantumsimulations_amd.problem import OBS_NAMES, time_grid
+    from quantumsimulations_amd.sweep import GAMMA_RARE, GAMMA_SEA, PHI, SWEEP_TOL, f_az_hz
+    from quantumsimulations_amd.sweep_runner import plan_sweep, write_sweep
+
+    def tree(root):
+        out = set()
+        for d, _, files in os.walk(root):
+            for f in files:
+                rel = os.path.relpath(os.path.join(d, f), root)
+                out.add(re.sub(r"sea_detuning_sweep_[0-9_]+", "S", rel))
+        return out
+
+    pages = {}
+    for w in (1, 3):
+        plan = plan_sweep(f_Az=f_az_hz(), f1A=20e3, target_sea_detuning=20e3, gamma_sea=GAMMA_SEA,
+                          gamma_rare=GAMMA_RARE, sea_detunings_Hz=np.linspace(0.0, 60e3, 8), n_sea=5,
+                          t_final=1e-4, steps=11, phi_sea=PHI, phi_rare=PHI,
+                          out_root=str(tmp_path / f"w{w}"), is_spin_three_half=False,
+                          coarse_window=2, verbose=False, **SWEEP_TOL)
+        traces = []
+        for i, p in enumerate(plan.flat):
+            t = time_grid(p)
+            obs = {k: np.cos(1e4 * t + j + 0.1 * i) for j, k in enumerate(OBS_NAMES)}
+            obs["Iz_sea"] = -1.0 + (1.0 + 0.05 * i) * t * 1e3
+            traces.append((t, obs))
+        base = write_sweep(plan, traces, report="full", verbose=False, workers=w)
+        pdf = open(os.path.join(base, "sea_detuning_report.pdf"), "rb").read()
+        pages[w] = pdf.count(b"/Type /Page") - pdf.count(b"/Type /Pages")
+    assert tree(tmp_path / "w1") == tree(tmp_path / "w3")
+    assert len([f for f in tree(tmp_path / "w3") if f.endswith(".png")]) >= 2 * 8
+    assert pages[1] == pages[3] > 8
