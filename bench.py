@@ -70,6 +70,8 @@ def parse():
                     help="persistent mode: output times propagated per launch from one Chebyshev series")
     ap.add_argument("--mixed-launch", type=int, default=int(os.environ.get("DSE_MIXED_LAUNCH", "0")),
                     help="persistent mode: 1- and 2-tile problems in one launch per interval (1)")
+    ap.add_argument("--obs-overlap", type=int, default=int(os.environ.get("DSE_OBS_OVERLAP", "0")),
+                    help="persistent mode: observables on a second stream per lane (1)")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
     ap.add_argument("--n-det", type=int, default=N_DET)
     ap.add_argument("--no-large", action="store_true", help="skip the config-5 single-GPU leg")
@@ -343,6 +345,7 @@ def main():
     eng.set_option("persistent", 0 if args.streaming else 1)
     eng.set_option("outputs_per_launch", args.outputs_per_launch)
     eng.set_option("mixed_launch", args.mixed_launch)
+    eng.set_option("obs_overlap", args.obs_overlap)
     if os.environ.get("DSE_CORESIDENT"):  # diagnostics: workgroups per 2-tile interval launch chunk
         eng.set_option("coresident", float(os.environ["DSE_CORESIDENT"]))
     for p in probs:

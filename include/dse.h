@@ -137,6 +137,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "time_kernels" 0 = off, N = bracket the step launches of every N-th interval with
  *                         HIP events (default 1)
  *          "max_degree"   Chebyshev degree cap per interval (default 2e6)
+ *          "obs_overlap"  persistent mode: 1 runs each interval group's observables on a second
+ *                         stream per lane (lowest priority) while the next group's launches run,
+ *                         with two sets of intermediate-output accumulators; 0 (default) in line
  *          "mixed_launch" persistent mode: 1 puts the 1- and 2-tile problems of one tile size in
  *                         one interval launch (stiffest pairs, 1-tile problems, remaining pairs)
  *                         when all 2-tile workgroups fit at once; 0 (default) one stream each

@@ -104,9 +104,12 @@ struct DevProb {
   double2* xslots;        // interval kernel, 2-tile problems: [2][kXSlots][2^L] hand-off slots
   // Multi-output launches: one interval-kernel launch propagates n_out <= n_acc consecutive output
   // times from a shared Chebyshev series.  Output j < n_out - 1 is accumulated in
-  // xacc[j << n_local], the last in the next psi buffer.
+  // xacc[j << n_local], the last in the next psi buffer.  With the observables overlapped
+  // (option obs_overlap) the launches of odd groups (q = 1) use the second set,
+  // xacc[(xacc_q + j) << n_local], so group g + 1 never writes what group g's observables read.
   double2* xacc;
   int n_acc;
+  int xacc_q;             // 0, or n_acc - 1: intermediate outputs per launch-parity set
 };
 
 // Coefficient row of output j of offset set `set`: kcap1 + 1 entries, row[0].x = the degree d of
@@ -168,7 +171,8 @@ hipError_t launch_basis_init(const BasisInit* list, int n_entries, uint64_t max_
 // observables of n_out outputs of a group (grid.y): output j < n_out - 1 from intermediate
 // accumulator j, the last from state buffer role bsel; output j's partials at partial + j * out_stride
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
-                      double* partial, hipStream_t st, int n_out = 1, size_t out_stride = 0);
+                      double* partial, hipStream_t st, int n_out = 1, size_t out_stride = 0,
+                      int xq = 0);  // xq: launch parity of the intermediate outputs (xacc_q set)
 // partial[2 * block + {0, 1}] = block sums of Re(conj(a) b) and |a|^2 over n amplitudes
 hipError_t launch_dot(const double2* a, const double2* b, size_t n, double* partial, int blocks,
                       hipStream_t st);

@@ -571,7 +571,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
     for (int j = 0; j < kMaxOut; ++j) {
       upd[j] = j < nj && coef_nterm(k, dj[j]) > 0;
       acc_j[j] = (j == n_out - 1) ? acc_t
-                                  : tile_rsrc(P.xacc + ((size_t)j << (L + P.tbl)) + (h << L), TBYTES);
+                                  : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << (L + P.tbl)) + (h << L), TBYTES);
     }
 #pragma unroll
     for (int r0 = 0; r0 < R; r0 += AB) {

@@ -166,7 +166,7 @@ k_step_generic(const DevProb* __restrict__ probs, const int2* __restrict__ items
 template <int L>
 __global__ void __launch_bounds__(Geo<L>::NT)
 k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bsel_last,
-      double* __restrict__ partial, size_t out_stride) {
+      double* __restrict__ partial, size_t out_stride, int xq) {
   using G = Geo<L>;
   constexpr int T = G::T, NT = G::NT, R = G::R;
   __shared__ double2 s_w[T];
@@ -182,7 +182,7 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
   // others in intermediate output j (bsel = 3 + j) of a multi-output launch
   const int bsel = (blockIdx.y == gridDim.y - 1) ? bsel_last : 3 + (int)blockIdx.y;
   partial += (size_t)blockIdx.y * out_stride;
-  const double2* psi = bsel < 3 ? P.buf[bsel] : P.xacc + ((size_t)(bsel - 3) << (L + P.tbl));
+  const double2* psi = bsel < 3 ? P.buf[bsel] : P.xacc + ((size_t)(xq * P.xacc_q + bsel - 3) << (L + P.tbl));
   const size_t base = (size_t)h << L;
 
   double2 own[R];
@@ -453,9 +453,9 @@ hipError_t launch_step_L(int mode, const DevProb* probs, const int2* items, int 
 
 template <int L>
 hipError_t launch_obs_L(const DevProb* probs, const int2* items, int n_items, int bsel,
-                        double* partial, hipStream_t st, int n_out, size_t out_stride) {
+                        double* partial, hipStream_t st, int n_out, size_t out_stride, int xq) {
   hipLaunchKernelGGL((k_obs<L>), dim3(n_items, n_out), dim3(Geo<L>::NT), 0, st, probs, items, bsel,
-                     partial, out_stride);
+                     partial, out_stride, xq);
   return hipGetLastError();
 }
 
@@ -505,12 +505,12 @@ hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items,
 }
 
 hipError_t launch_obs(int L, const DevProb* probs, const int2* items, int n_items, int bsel,
-                      double* partial, hipStream_t st, int n_out, size_t out_stride) {
+                      double* partial, hipStream_t st, int n_out, size_t out_stride, int xq) {
   if (n_items <= 0 || n_out <= 0) return hipSuccess;
   if (n_out > 1 && bsel >= 3) return hipErrorInvalidValue;
   switch (L) {
 #define X(l) \
-  case l: return launch_obs_L<l>(probs, items, n_items, bsel, partial, st, n_out, out_stride);
+  case l: return launch_obs_L<l>(probs, items, n_items, bsel, partial, st, n_out, out_stride, xq);
     DSE_TILE_CASES(X)
 #undef X
     default: return hipErrorInvalidValue;

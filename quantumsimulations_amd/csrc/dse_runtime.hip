@@ -89,6 +89,12 @@ struct LaneGroup {
 };
 struct Lane {
   hipStream_t stream = nullptr;
+  // persistent mode, option obs_overlap: the observables of interval group g run on obs_stream
+  // behind ev_iv[g & 1] (its interval launches), and interval group g + 2, which rewrites the
+  // buffers they read, waits for ev_obs[g & 1]
+  hipStream_t obs_stream = nullptr;
+  hipEvent_t ev_iv[2] = {nullptr, nullptr}, ev_obs[2] = {nullptr, nullptr};
+  bool obs_pending[2] = {false, false};
   std::vector<LaneGroup> groups;
   std::vector<hipEvent_t> ev[2];
   size_t ev_used[2] = {0, 0};
@@ -124,6 +130,7 @@ struct dse_ctx {
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
   int mixed_launch = 0;             // persistent: 1- and 2-tile problems of one tile size in one launch
+  int obs_overlap = 0;              // persistent: observables off the interval launches' stream
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
   int handoff_fallbacks = 0;        // evolves re-run on the streaming kernels after a hand-off timeout
@@ -300,8 +307,14 @@ void destroy_lanes(dse_ctx* ctx) {
   }
   for (auto& ln : ctx->lanes) {
     if (ln.stream) (void)hipStreamSynchronize(ln.stream);
+    if (ln.obs_stream) (void)hipStreamSynchronize(ln.obs_stream);
     for (auto& pool : ln.ev)
       for (auto e : pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+      if (ln.ev_iv[i]) (void)hipEventDestroy(ln.ev_iv[i]);
+      if (ln.ev_obs[i]) (void)hipEventDestroy(ln.ev_obs[i]);
+    }
+    if (ln.obs_stream) (void)hipStreamDestroy(ln.obs_stream);
     if (ln.stream) (void)hipStreamDestroy(ln.stream);
   }
   ctx->lanes.clear();
@@ -311,13 +324,27 @@ int ensure_lanes(dse_ctx* ctx) {
   if ((int)ctx->lanes.size() == ctx->n_streams) return DSE_OK;
   destroy_lanes(ctx);
   ctx->lanes.resize(ctx->n_streams);
-  for (auto& ln : ctx->lanes) HIPC(hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
+  for (auto& ln : ctx->lanes) {
+    HIPC(hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
+    // lowest priority: the observables take the CUs the next interval launch leaves, not the
+    // other way round
+    int least = 0, greatest = 0;
+    HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPC(hipStreamCreateWithPriority(&ln.obs_stream, hipStreamNonBlocking, least));
+    for (int i = 0; i < 2; ++i) {
+      HIPC(hipEventCreateWithFlags(&ln.ev_iv[i], hipEventDisableTiming));
+      HIPC(hipEventCreateWithFlags(&ln.ev_obs[i], hipEventDisableTiming));
+    }
+  }
   return DSE_OK;
 }
 
 int sync_all(dse_ctx* ctx) {
   if (ctx->swap_stream) HIPC(hipStreamSynchronize(ctx->swap_stream));
-  for (auto& ln : ctx->lanes) HIPC(hipStreamSynchronize(ln.stream));
+  for (auto& ln : ctx->lanes) {
+    HIPC(hipStreamSynchronize(ln.stream));
+    if (ln.obs_stream) HIPC(hipStreamSynchronize(ln.obs_stream));
+  }
   if (ctx->small_stream) HIPC(hipStreamSynchronize(ctx->small_stream));
   return DSE_OK;
 }
@@ -1065,6 +1092,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     ctx->xcd_pairs = value != 0.0;
   } else if (k == "mixed_launch") {
     ctx->mixed_launch = value != 0.0;
+  } else if (k == "obs_overlap") {
+    ctx->obs_overlap = value != 0.0;
   } else if (k == "time_kernels") {
     if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
     ctx->time_every = (int)value;
@@ -1716,6 +1745,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     d.beta = beta;
     d.s1 = 1.0 / alpha;
     d.n_acc = M;
+    d.xacc_q = (persistent && ctx->obs_overlap) ? M - 1 : 0;
   };
   if (ctx->dbg & 4)
     for (size_t pi = 0; pi < ctx->probs.size(); ++pi) coef_one(pi);
@@ -1746,12 +1776,15 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   }
 
   phase("coef upload");
-  // intermediate outputs of multi-output launches: (M - 1) state vectors per problem
+  // intermediate outputs of multi-output launches: (M - 1) state vectors per problem, two sets
+  // (one per launch parity) when the observables are overlapped
+  const bool obs_ovl = persistent && ctx->obs_overlap;
   {
+    const size_t xsets = obs_ovl ? 2 : 1;
     size_t need = 0;
     if (M > 1)
       for (auto& P : ctx->probs)
-        if (!P.sm) need += (size_t)(M - 1) << P.n_local;
+        if (!P.sm) need += xsets * ((size_t)(M - 1) << P.n_local);
     if (need > ctx->xacc_cap) {
       if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
       ctx->xacc_cap = 0;
@@ -1764,7 +1797,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
       const bool use = M > 1 && !ctx->probs[pi].sm;
       ctx->h_desc[pi].xacc = use ? ctx->d_xacc + off : nullptr;
-      if (use) off += (size_t)(M - 1) << ctx->probs[pi].n_local;
+      if (use) off += xsets * ((size_t)(M - 1) << ctx->probs[pi].n_local);
     }
   }
 
@@ -2048,19 +2081,33 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   };
   // observables of n_out consecutive output slots (one launch per lane group): outputs
   // j < n_out - 1 from the intermediate accumulators, the last from state role bsel_q
-  auto obs_all = [&](int bsel_q, size_t slot, int n_out) -> int {
-    for (auto& ln : ctx->lanes)
+  // obs_ovl: on each lane's obs_stream behind the lane's interval launches of parity xq (event
+  // ev_iv[xq]), then ev_obs[xq] for the launches two groups later, which rewrite these buffers
+  auto obs_all = [&](int bsel_q, size_t slot, int n_out, int xq) -> int {
+    for (auto& ln : ctx->lanes) {
+      if (ln.groups.empty()) continue;
+      hipStream_t os = obs_ovl ? ln.obs_stream : ln.stream;
+      if (obs_ovl) {
+        HIPC(hipEventRecord(ln.ev_iv[xq], ln.stream));
+        HIPC(hipStreamWaitEvent(os, ln.ev_iv[xq], 0));
+      }
       for (auto& g : ln.groups)
         HIPC(launch_obs(g.L, ctx->d_probs, ctx->d_items + g.off, (int)g.count, bsel_q,
-                        ctx->d_partial + (slot * ctx->total_items + g.off) * 8, ln.stream, n_out,
-                        (size_t)ctx->total_items * 8));
+                        ctx->d_partial + (slot * ctx->total_items + g.off) * 8, os, n_out,
+                        (size_t)ctx->total_items * 8, xq));
+      if (obs_ovl) {
+        HIPC(hipEventRecord(ln.ev_obs[xq], os));
+        ln.obs_pending[xq] = true;
+      }
+    }
     return DSE_OK;
   };
+  for (auto& ln : ctx->lanes) ln.obs_pending[0] = ln.obs_pending[1] = false;
 
   std::vector<double> dist_raw(any_dist ? ctx->probs.size() * (size_t)n_t * 7 : 0, 0.0);
   size_t slot = 0, t_flushed = 0;
   if (any_dist && (rc = dist_exchange(ctx, 0, 0, ctx->lanes[0].stream))) return rc;
-  if ((rc = obs_all(0, slot++, 1))) return rc;
+  if ((rc = obs_all(0, slot++, 1, 1))) return rc;
   for (int gi = 0; gi < n_groups; ++gi) {
     const Group& G = groups[gi];
     const int q = gi & 1;
@@ -2071,6 +2118,10 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
       Lane& ln = ctx->lanes[li];
       if (ln.groups.empty()) continue;
       if ((rc = drain(ln, li, pool))) return rc;
+      if (obs_ovl && ln.obs_pending[q]) {  // the observables that read what this group rewrites
+        HIPC(hipStreamWaitEvent(ln.stream, ln.ev_obs[q], 0));
+        ln.obs_pending[q] = false;
+      }
       for (auto& g : ln.groups) {
         const int T = 1 << g.L;
         if (persistent) {
@@ -2150,9 +2201,10 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
           for (auto& g : ln.groups)
             HIPC(launch_obs(g.L, ctx->d_probs, ctx->d_items + g.off, (int)g.count,
                             j == G.n_out - 1 ? (q ? 0 : 2) : 3 + j,
-                            ctx->d_partial + ((slot + j) * ctx->total_items + g.off) * 8, ln.stream));
+                            ctx->d_partial + ((slot + j) * ctx->total_items + g.off) * 8, ln.stream,
+                            1, 0, q));
       }
-    } else if ((rc = obs_all(q ? 0 : 2, slot, G.n_out))) {
+    } else if ((rc = obs_all(q ? 0 : 2, slot, G.n_out, q))) {
       return rc;
     }
     slot += G.n_out;

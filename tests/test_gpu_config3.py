@@ -157,3 +157,31 @@ def test_mixed_launch_is_bitwise_identical(engine):
             assert np.array_equal(obs, res[mixed])
         res[mixed] = obs
     assert np.array_equal(res[1], res[0])
+
+
+@pytest.mark.parametrize("m", [2, 1])
+def test_overlapped_observables_are_bitwise_identical(engine, m):
+    """Option obs_overlap (default off): the observables of each interval launch run on a second
+    stream per lane while the next launch runs, and the multi-output launches alternate between two
+    sets of intermediate accumulators.  The arithmetic is unchanged, so the results are bitwise
+    those of the in-line schedule, also when repeated in one context and over several flushes."""
+    t = np.linspace(0.0, 2e-4, 41)
+    res = {}
+    for ovl in (1, 0, 1):
+        engine.clear()
+        engine.set_option("obs_overlap", ovl)
+        engine.set_option("outputs_per_launch", m)
+        try:
+            for variant in VARIANTS:
+                for delta in DELTAS:
+                    engine.add(pb.build_problem(_params(variant, delta, t)))
+            obs, st = engine.evolve(t)
+        finally:
+            engine.set_option("obs_overlap", 0)
+            engine.set_option("outputs_per_launch", 2)
+            engine.clear()
+        assert st["mode"] == 1 and st["outputs_per_launch"] == m
+        if ovl in res:
+            assert np.array_equal(obs, res[ovl])
+        res[ovl] = obs
+    assert np.array_equal(res[1], res[0])
