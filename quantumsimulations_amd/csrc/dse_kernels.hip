@@ -208,22 +208,48 @@ k_obs(const DevProb* __restrict__ probs, const int2* __restrict__ items, int bse
       acc[2] += p2 * (half_sea - (double)__popcll(x & P.sea_mask));
       if (P.rare_bit >= 0) acc[3] += p2 * (0.5 - (double)((x >> P.rare_bit) & 1ull));
     }
-    for (int b = 0; b < P.n; ++b) {
+    // in-tile bits, unrolled: a register bit's partner is another row of this thread (no LDS
+    // read, rows chosen at compile time), a thread bit's rows are all this lane's or none; same
+    // rows in the same order as a per-row test, so the sums are bitwise unchanged
+    constexpr int TB = G::TB;
+#pragma unroll
+    for (int b = 0; b < L; ++b) {
+      if (b >= P.n) break;
       const bool sea = (P.sea_mask >> b) & 1ull;
       const bool rr = (b == P.rare_bit);
       if (!sea && !rr) continue;
       double ore = 0.0, oim = 0.0;
-      if (b < L) {
+      if (b >= TB) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const uint32_t x = (uint32_t)(r * NT + tid);
-          if (!((x >> b) & 1u)) {
-            const double2 s = s_w[x ^ (1u << b)];
-            ore += own[r].x * s.x + own[r].y * s.y;
-            oim += own[r].x * s.y - own[r].y * s.x;
-          }
+          if ((r >> (b - TB)) & 1) continue;
+          const double2 s = own[r ^ (1 << (b - TB))];
+          ore += own[r].x * s.x + own[r].y * s.y;
+          oim += own[r].x * s.y - own[r].y * s.x;
         }
-      } else {
+      } else if (!((tid >> b) & 1)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double2 s = s_w[(uint32_t)(r * NT + tid) ^ (1u << b)];
+          ore += own[r].x * s.x + own[r].y * s.y;
+          oim += own[r].x * s.y - own[r].y * s.x;
+        }
+      }
+      if (sea) {
+        acc[0] += ore;
+        acc[1] += oim;
+      }
+      if (rr) {
+        acc[4] += ore;
+        acc[5] += oim;
+      }
+    }
+    for (int b = L; b < P.n; ++b) {
+      const bool sea = (P.sea_mask >> b) & 1ull;
+      const bool rr = (b == P.rare_bit);
+      if (!sea && !rr) continue;
+      double ore = 0.0, oim = 0.0;
+      {
         if ((hg >> (b - L)) & 1u) continue;
         const uint32_t hp = hg ^ (1u << (b - L));
         // intermediate outputs (bsel >= 3) live only in this context, unsharded
