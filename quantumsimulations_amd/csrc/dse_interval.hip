@@ -153,6 +153,9 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   __shared__ IvShared<L> S;
   __shared__ int s_fail;
 
+  // a hand-off of an earlier launch timed out: this evolve is abandoned (the runtime re-runs it on
+  // the streaming kernels), so launches queued behind that one return at once
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
   const uint32_t h = (uint32_t)it.y;
@@ -521,7 +524,9 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
           const int limit = g_dse_spin_limit;
           while (limit < 0 || __hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
             __builtin_amdgcn_s_sleep(1);
-            if (limit < 0 || ++spins > limit) {
+            // give up at the limit, or as soon as another pair has (its partner may never come)
+            if (limit < 0 || ++spins > limit ||
+                ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
               s_fail = 1;
               atomicExch(err, 1);
               break;
@@ -532,6 +537,9 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
         }
+      // compiler barrier: the operand loads below stay behind the poll in program order (one wave
+      // issues its memory instructions in order, so the hardware keeps them there too)
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         double2 uv[NH];

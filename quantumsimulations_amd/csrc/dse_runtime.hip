@@ -103,6 +103,9 @@ struct Lane {
 
 }  // namespace
 
+// internal return code of evolve_impl: a persistent hand-off timed out (dse_evolve falls back)
+constexpr int kRcHandoffTimeout = 1000;
+
 struct dse_ctx {
   int device = 0;
   std::string err;
@@ -133,7 +136,10 @@ struct dse_ctx {
   int obs_overlap = 0;              // persistent: observables off the interval launches' stream
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
-  int handoff_fallbacks = 0;        // evolves re-run on the streaming kernels after a hand-off timeout
+  int handoff_fallbacks = 0;        // this evolve call re-ran on the streaming kernels after a hand-off timeout (0/1)
+  int* d_err_cur = nullptr;         // the hand-off error word of the running persistent evolve (else null)
+  double* d_allreduce = nullptr;    // RCCL all-reduce staging buffer of the observable sums (grow-only)
+  size_t allreduce_cap = 0;         // in doubles
   int* d_flags = nullptr;           // hand-off flags (2 tiles x kIvWaves per problem) + error word
   size_t flags_cap = 0;
   double2* d_xslots = nullptr;      // hand-off slots of the interval kernel
@@ -285,6 +291,8 @@ void free_device(dse_ctx* ctx) {
   if (ctx->d_small_out) (void)hipFree(ctx->d_small_out), ctx->d_small_out = nullptr;
   if (ctx->d_small_aux) (void)hipFree(ctx->d_small_aux), ctx->d_small_aux = nullptr;
   ctx->small_cap = ctx->small_out_cap = ctx->small_aux_cap = 0;
+  if (ctx->d_allreduce) (void)hipFree(ctx->d_allreduce), ctx->d_allreduce = nullptr;
+  ctx->allreduce_cap = 0;
   ctx->zzlo_tables.clear();
   ctx->partial_slots = 0;
   ctx->total_items = 0;
@@ -335,6 +343,17 @@ int ensure_lanes(dse_ctx* ctx) {
       HIPC(hipEventCreateWithFlags(&ln.ev_iv[i], hipEventDisableTiming));
       HIPC(hipEventCreateWithFlags(&ln.ev_obs[i], hipEventDisableTiming));
     }
+  }
+  return DSE_OK;
+}
+
+// the interval / step / observable streams (not the small-register engine's, which small_gather
+// waits for): what flush_partials needs before it reads the observable partials
+int sync_lanes(dse_ctx* ctx) {
+  if (ctx->swap_stream) HIPC(hipStreamSynchronize(ctx->swap_stream));
+  for (auto& ln : ctx->lanes) {
+    HIPC(hipStreamSynchronize(ln.stream));
+    if (ln.obs_stream) HIPC(hipStreamSynchronize(ln.obs_stream));
   }
   return DSE_OK;
 }
@@ -749,13 +768,18 @@ int xchg_allreduce_host(dse_ctx* ctx, double* v, size_t count, hipStream_t st) {
       return fail(ctx, DSE_ERR_HIP, "exchange callback (all-reduce) failed");
     return DSE_OK;
   }
-  double* d = nullptr;
-  HIPC(hipMalloc(&d, count * sizeof(double)));
+  if (ctx->allreduce_cap < count) {  // one staging buffer per context, grown on demand
+    if (ctx->d_allreduce) (void)hipFree(ctx->d_allreduce), ctx->d_allreduce = nullptr;
+    ctx->allreduce_cap = 0;
+    if (hipMalloc(&ctx->d_allreduce, count * sizeof(double)) != hipSuccess)
+      return fail(ctx, DSE_ERR_OOM, "all-reduce staging allocation failed");
+    ctx->allreduce_cap = count;
+  }
+  double* d = ctx->d_allreduce;
   hipError_t e = hipMemcpyAsync(d, v, count * sizeof(double), hipMemcpyHostToDevice, st);
   const ncclResult_t r = ncclAllReduce(d, d, count, ncclFloat64, ncclSum, ctx->comm, st);
   if (e == hipSuccess) e = hipMemcpyAsync(v, d, count * sizeof(double), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  (void)hipFree(d);
   if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   HIPC(e);
   return DSE_OK;
@@ -873,7 +897,12 @@ void finish_obs(const HostProblem& P, const double* v, double* o, size_t stride)
 // dist_raw for the all-reduce at the end of dse_evolve.
 int flush_partials(dse_ctx* ctx, size_t nslots, size_t t0, int n_t, double* obs_out,
                    std::vector<double>* dist_raw) {
-  if ((int)sync_all(ctx)) return DSE_ERR_HIP;
+  if ((int)sync_lanes(ctx)) return DSE_ERR_HIP;
+  if (ctx->d_err_cur) {  // a persistent hand-off timed out: abandon this run (dse_evolve falls back)
+    int herr = 0;
+    HIPC(hipMemcpy(&herr, ctx->d_err_cur, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr) return kRcHandoffTimeout;
+  }
   std::vector<double> h(nslots * ctx->total_items * 8);
   HIPC(hipMemcpy(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost));
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
@@ -1587,8 +1616,7 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
   return DSE_OK;
 }
 
-int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
-  if (!ctx) return DSE_ERR_ARG;
+static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
   const auto wall0 = std::chrono::steady_clock::now();
   // DSE_HOST_TIMING=1: host time of each phase of this call on stderr (diagnostics)
   static const bool host_timing = std::getenv("DSE_HOST_TIMING") != nullptr;
@@ -2001,6 +2029,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     HIPC(hipMemset(ctx->d_flags, 0, need * sizeof(int)));
   }
   int* d_err = persistent ? ctx->d_flags + 2 * kIvWaves * ctx->probs.size() : nullptr;
+  ctx->d_err_cur = d_err;  // checked by every flush_partials (reset by dse_evolve on return)
 
   phase("lanes/items");
   // ---- psi(t0) = |psi0> ----
@@ -2228,21 +2257,7 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   if (persistent && any_big) {
     int herr = 0;
     HIPC(hipMemcpy(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (herr) {
-      // A workgroup pair of a 2-tile problem was not resident together within the spin limit
-      // (the device shared with long-running work of another stream or process): the results of
-      // this call are incomplete, so it runs again on the per-term streaming kernels, which have
-      // no inter-workgroup dependency.
-      const int zero = 0;
-      HIPC(hipMemcpy(d_err, &zero, sizeof(int), hipMemcpyHostToDevice));
-      const int saved = ctx->persistent;
-      ctx->persistent = 0;
-      ctx->handoff_fallbacks += 1;
-      rc = dse_evolve(ctx, t, n_t, tol, obs_out, stats);
-      ctx->persistent = saved;
-      if (stats) stats->handoff_fallbacks = ctx->handoff_fallbacks;
-      return rc;
-    }
+    if (herr) return kRcHandoffTimeout;
   }
   if (any_dist) {  // sums over all shards of the register, then normalisation (finish_obs)
     if ((rc = xchg_allreduce_host(ctx, dist_raw.data(), dist_raw.size(), ctx->lanes[0].stream))) return rc;
@@ -2286,6 +2301,31 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
     stats->exchange_bytes = ctx->xbytes;
   }
   return DSE_OK;
+}
+
+int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
+  if (!ctx) return DSE_ERR_ARG;
+  ctx->handoff_fallbacks = 0;
+  int rc = evolve_impl(ctx, t, n_t, tol, obs_out, stats);
+  int* const d_err = ctx->d_err_cur;
+  ctx->d_err_cur = nullptr;
+  if (rc != kRcHandoffTimeout) return rc;
+  // A workgroup pair of a 2-tile problem was not resident together within the spin limit (the
+  // device shared with long-running work of another stream or process).  The first flush after
+  // the timeout saw it (launches queued behind it return at once: k_interval checks the error
+  // word on entry), so the call runs again on the per-term streaming kernels, which have no
+  // inter-workgroup dependency.
+  (void)sync_all(ctx);
+  const int zero = 0;
+  HIPC(hipMemcpy(d_err, &zero, sizeof(int), hipMemcpyHostToDevice));
+  const int saved = ctx->persistent;
+  ctx->persistent = 0;
+  rc = evolve_impl(ctx, t, n_t, tol, obs_out, stats);
+  ctx->persistent = saved;
+  ctx->d_err_cur = nullptr;
+  ctx->handoff_fallbacks = 1;
+  if (stats) stats->handoff_fallbacks = 1;
+  return rc;
 }
 
 int dse_get_state(dse_ctx* ctx, int problem, double* psi_out) {

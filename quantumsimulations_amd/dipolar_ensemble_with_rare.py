@@ -82,6 +82,7 @@ def simulate_rare_batch(params_list: Sequence[DipolarRareParams], device: int | 
     from .engine import batches_for_memory, evolve_groups
     by_grid = evolve_groups([(float(p.t_final), int(p.steps)) for p in params_list], probs)
     for key, idxs in by_grid.items():
+        eng.clear()  # free the previous group's buffers before sizing this group's batches
         for batch in batches_for_memory([probs[i] for i in idxs], device):
             members = [idxs[b] for b in batch]
             eng.clear()

@@ -59,11 +59,19 @@ def evolve_groups(grid_keys, probs) -> Dict[Tuple, list]:
     return groups
 
 
+# Device memory a context holds besides its problems: observable partials (up to 256 MiB), the
+# intermediate outputs and hand-off slots of the interval kernel beyond the per-problem estimate,
+# flags, coefficient arenas.
+CONTEXT_BYTES = 512 << 20
+
+
 def batches_for_memory(probs, device: int, headroom: float = 0.8):
     """Index batches of ``probs`` whose summed footprint fits ``headroom`` of the free memory of
-    ``device`` (at least one problem per batch; a problem too large alone still gets its own)."""
+    ``device`` less one context's fixed arenas (at least one problem per batch; a problem too large
+    alone still gets its own).  Call it with the context cleared, so its last batch's buffers are
+    not counted as used."""
     free, _ = device_memory(device)
-    budget = headroom * free
+    budget = headroom * free - CONTEXT_BYTES
     out, cur, used = [], [], 0.0
     for i, p in enumerate(probs):
         b = problem_bytes(p)

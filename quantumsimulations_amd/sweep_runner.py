@@ -72,6 +72,14 @@ def assign_lpt(costs: Sequence[float], n_bins: int) -> List[List[int]]:
 # DSE_ENGINE_CACHE=0 opens and closes a context per call, as before.
 _ENGINES: Dict[Tuple[type, int], Any] = {}
 _ENGINES_LOCK = threading.Lock()
+# A cached context is not thread-safe (include/dse.h): whoever uses one holds its lock for the whole
+# clear / add / evolve sequence, so duplicate device ids or concurrent evolve_many calls serialise.
+_ENGINE_USE: Dict[Tuple[type, int], threading.Lock] = {}
+
+
+def _use_lock(cls, dev: int) -> threading.Lock:
+    with _ENGINES_LOCK:
+        return _ENGINE_USE.setdefault((cls, dev), threading.Lock())
 
 
 def _engine_for(cls, dev: int):
@@ -119,6 +127,11 @@ def evolve_many(params_list: Sequence[DipolarRareParams], devices: Optional[Sequ
     errors: List[BaseException] = []
 
     def work(dev: int, idxs: List[int]) -> None:
+        from .engine import Engine
+        with _use_lock(Engine, dev):
+            _work(dev, idxs)
+
+    def _work(dev: int, idxs: List[int]) -> None:
         from .engine import Engine, batches_for_memory, evolve_groups
         eng, own = None, False
         try:
