@@ -20,10 +20,17 @@ Extra fields of the JSON line:
                  rate alongside; "traffic" = the counter-measured bytes per launch
                  (profiles/<round>/bench_pmc_traffic.json)
   full_sweep     the reference's own grid (t_final 30 s, 20000 outputs, sweep_sea_detuning.py:
-                 1223-1224) on the same 64 x 3 evolutions: the first few output intervals timed,
-                 extrapolated to all 19999 -> points/hour and ms per ODE step
+                 1223-1224) on the same 64 x 3 evolutions: the first 16 output intervals timed 3
+                 times (spread reported), extrapolated to all 19999 -> points/hour and ms per ODE
+                 step: BASELINE's "(full sweep)" figure (`value` is the 1 ms head-to-head grid)
   cpu_baseline   rank 0, N = 1 only: the QuTiP-5 sesolve equivalent (oracle/cpu_bench.py) on
-                 the host cores, 1 core and all cores, run before the GPU is touched
+                 the host cores, 1 core, this job's CPU share and a node-wide estimate, run
+                 before the GPU is touched
+  config2        rank 0, N = 1 only: BASELINE config 2 (one N = 12 evolution, 2 ms / 201 outputs)
+                 through the drop-in simulate_rare, and the unmodified caller's three serial
+                 calls per point at N = 14
+  reference_default  rank 0, N = 1 only: the reference's own default run (N = 7, 13 detunings x
+                 3 variants, 30 s / 20 000 outputs) timed whole on the dense eigen-propagator
   large_register rank 0, N = 1 only: config 5 on one GPU (N = 30, Walsh-Hadamard engine) against
                  the HBM roofline, with exact-invariant checks (norm, energy); --no-large skips it
   partitioned    N = 2, 4, 8 only, after the timed sweep: config 5 with the N = 30 register split
@@ -62,7 +69,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tile-bits", type=int, default=int(os.environ.get("DSE_TILE_BITS", "13")))
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DSE_STREAMS", "4")))
-    ap.add_argument("--cpu-budget", type=float, default=float(os.environ.get("DSE_CPU_BUDGET_S", "20")))
+    ap.add_argument("--cpu-fraction", type=float, default=float(os.environ.get("DSE_CPU_FRACTION", "0.25")),
+                    help="share of the 1 ms grid each CPU-baseline evolution integrates")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streaming", action="store_true", help="per-term streaming kernels instead of "
                     "the persistent interval kernel")
@@ -76,8 +84,13 @@ def parse():
     ap.add_argument("--n-det", type=int, default=N_DET)
     ap.add_argument("--no-large", action="store_true", help="skip the config-5 single-GPU leg")
     ap.add_argument("--no-full", action="store_true", help="skip the reference-grid (30 s) leg")
-    ap.add_argument("--full-intervals", type=int, default=2,
+    ap.add_argument("--full-intervals", type=int, default=16,
                     help="output intervals of the 30 s reference grid timed by the full-sweep leg")
+    ap.add_argument("--full-repeats", type=int, default=3,
+                    help="timed runs of those intervals (their spread is reported)")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 / serial-caller leg")
+    ap.add_argument("--no-refdefault", action="store_true",
+                    help="skip the reference-default (N = 7, 30 s grid) leg")
     ap.add_argument("--partitioned-timeout", type=float, default=180.0,
                     help="N > 1: seconds allowed for the config-5 partitioned leg (child processes)")
     ap.add_argument("--cpu-cores", type=int, default=int(os.environ.get("DSE_CPU_CORES", "0")),
@@ -112,7 +125,7 @@ def flops_per_amp(prob) -> float:
     return 4.0 + 8.0 * n_flips + 2.0 * n_pairs
 
 
-def cpu_baseline(budget_s: float, cores: int):
+def cpu_baseline(fraction: float, cores: int):
     """QuTiP-5 sesolve equivalent on the host cores (oracle/cpu_bench.py), run as a child process
     before this process touches the GPU (its worker pool forks a process without a GPU context)."""
     import subprocess
@@ -122,9 +135,9 @@ def cpu_baseline(budget_s: float, cores: int):
             if os.environ.get(key, "").isdigit():
                 cores = min(cores, int(os.environ[key]))
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    res = subprocess.run([sys.executable, "-m", "oracle.cpu_bench", "--budget", str(budget_s),
+    res = subprocess.run([sys.executable, "-m", "oracle.cpu_bench", "--fraction", str(fraction),
                           "--cores", str(cores)], cwd=ROOT, env=env, capture_output=True, text=True,
-                         timeout=max(600.0, 20.0 * budget_s))
+                         timeout=900.0)
     if res.returncode != 0:
         raise RuntimeError(f"oracle.cpu_bench failed: {res.stderr[-2000:]}")
     return json.loads(res.stdout.strip().splitlines()[-1])
@@ -193,25 +206,30 @@ def large_register(device: int, n_sea: int = 29):
     }
 
 
-def full_sweep(eng, probs, n_points: int, intervals: int, sync, dist=None):
+def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, dist=None):
     """The reference's grid (sweep_sea_detuning.py:1223-1224: t_final 30 s, 20000 outputs ->
     dt = 1.5 ms, alpha dt ~ 3e3..1e4: one output per launch, ~1e4 Chebyshev terms each) on the
-    bench's evolutions: one interval untimed (coefficients, warm-up), then the first `intervals`
-    output intervals timed (barrier + device sync around, max over ranks) and extrapolated
-    linearly to all 19999 intervals (every interval has the same length, so the same work)."""
+    bench's evolutions: one interval untimed (coefficients, warm-up), then `repeats` timed runs of
+    the first `intervals` output intervals (barrier + device sync around each, max over ranks),
+    extrapolated linearly to all 19999 intervals (every interval has the same length, so the same
+    work); the spread over the repeats is reported."""
     t_ref = np.linspace(0.0, 30.0, 20000)
     eng.evolve(t_ref[:2])
-    stats = []
-    dt = timed_steps(lambda: stats.append(eng.evolve(t_ref[:intervals + 1])[1]), 1, 0, sync, dist)
+    stats, per = [], []
+    for _ in range(max(1, repeats)):
+        dt = timed_steps(lambda: stats.append(eng.evolve(t_ref[:intervals + 1])[1]), 1, 0, sync, dist)
+        per.append(dt / intervals)
     st = stats[-1]
-    per_interval = dt / intervals
+    per_interval = float(np.mean(per))
     full_s = per_interval * (len(t_ref) - 1)
     h_per_ev = st["h_applications"] / len(probs) / intervals     # H applications per evolution
     k_ms = st["step_kernel_ms"]
     gbs = 80.0 * st["timed_amp_terms"] / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     return {
         "grid": "t_final 30 s, 20000 outputs (sweep_sea_detuning.py:1223-1224)",
-        "intervals_timed": intervals, "s_per_interval": per_interval,
+        "intervals_timed": intervals, "repeats": len(per), "s_per_interval": per_interval,
+        "s_per_interval_min": float(np.min(per)), "s_per_interval_max": float(np.max(per)),
+        "spread_rel": float((np.max(per) - np.min(per)) / per_interval),
         "full_sweep_s_extrapolated": full_s,
         "value": n_points * 3600.0 / full_s, "unit": "detuning-points/hour (extrapolated)",
         "ms_per_ode_step": per_interval * 1e3 / h_per_ev,
@@ -220,8 +238,100 @@ def full_sweep(eng, probs, n_points: int, intervals: int, sync, dist=None):
         "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(st["mode"], "streaming"),
         "kernel_gbs_80B_per_amp_term": gbs,
         "kernel_frac_hbm": gbs / HBM_PEAK_GBS if gbs else None,
-        "note": "extrapolated from the timed intervals; the reference's own ZVODE trace of this grid "
-                "takes ~430-1530 h per N=14 evolution on one core (SURVEY.md §6)",
+        "note": "the BASELINE '(full sweep)' figure: this grid, extrapolated from the timed intervals "
+                "(headline `value` is the 1 ms head-to-head grid); the reference's own ZVODE trace of "
+                "this grid takes ~430-1530 h per N=14 evolution on one core (SURVEY.md §6)",
+    }
+
+
+def config2_leg(device: int):
+    """BASELINE config 2 through the drop-in surface: one N = 12 center_on evolution (n_sea = 11,
+    50 kHz, 2 ms / 201 outputs) by simulate_rare (dipolar_ensemble_with_rare.py:611 replaced), wall
+    time per call after a warm-up call, and its distance to the exact-eigh fixture of the
+    reference-built H (tests/golden/traces_n12.npz, data only).  Then the unmodified caller's
+    pattern at N = 14 (sweep_sea_detuning.py:671-702: three serial simulate_rare calls per point,
+    1 ms / 101 outputs, 75 kHz)."""
+    os.environ.setdefault("DSE_DEVICE", str(device))
+    from quantumsimulations_amd import dipolar_ensemble_with_rare as dse
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.engine import Engine
+    from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
+    p = sweep_point_params(11, 50e3, "center_on", 2e-3, 201)
+    dse.simulate_rare(p)
+    walls, res = [], None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        res = dse.simulate_rare(p)
+        walls.append((time.perf_counter() - t0) * 1e3)
+    err = None
+    try:
+        tr = np.load(os.path.join(ROOT, "tests", "golden", "traces_n12.npz"), allow_pickle=False)
+        err = max(float(np.max(np.abs(res[1][k] - tr[f"exact_{k}"]))) for k in res[1])
+    except (OSError, KeyError):
+        pass
+    with Engine(device) as eng:   # the engine's own counters for the same evolution
+        eng.add(pb.build_problem(p))
+        eng.evolve(pb.time_grid(p))
+        _, st = eng.evolve(pb.time_grid(p))
+    ps = [sweep_point_params(13, 75e3, v, 1e-3, 101) for v in VARIANTS]
+    for q in ps:
+        dse.simulate_rare(q)
+    t0 = time.perf_counter()
+    for q in ps:
+        dse.simulate_rare(q)
+    serial14 = (time.perf_counter() - t0) * 1e3
+    return {
+        "workload": "config 2: N=12 (n_sea=11) center_on, 50 kHz, t_final 2 ms, 201 outputs, one "
+                    "simulate_rare call",
+        "wall_ms": float(np.median(walls)), "wall_ms_runs": walls,
+        "max_abs_err_vs_exact": err, "tolerance": 1e-8,
+        "engine": {"mode": st["mode"], "max_degree": st["max_degree"],
+                   "h_applications": st["h_applications"], "launches": st["step_launches"],
+                   "kernel_ms": st["step_kernel_ms"], "dense_problems": st["dense_problems"]},
+        "ms_per_h_application": float(np.median(walls)) / max(st["h_applications"], 1),
+        "unmodified_caller_n14": {"calls": 3, "grid": "1 ms / 101 outputs, 75 kHz",
+                                  "wall_ms": serial14, "ms_per_call": serial14 / 3},
+    }
+
+
+def reference_default_leg(device: int, k_cheb: int = 20):
+    """The reference's own default run (sweep_sea_detuning.py:1223-1240: n_sea = 6 -> N = 7, 13
+    detunings in [0, 150 kHz] x 3 variants, t_final 30 s, 20 000 outputs), all 39 evolutions in one
+    evolve: the engine's cost model takes the dense eigen-propagator (every output exact at any
+    time).  Timed whole (after one untimed call), no extrapolation.  Beside it, the Chebyshev
+    small-register engine (option dense = 0) on the first `k_cheb` intervals, extrapolated."""
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.engine import Engine
+    from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
+    t_ref = np.linspace(0.0, 30.0, 20000)
+    dets = np.linspace(0.0, 150e3, 13)
+    probs = [pb.build_problem(sweep_point_params(6, float(d), v, 30.0, 20000)) for d in dets for v in VARIANTS]
+    with Engine(device) as eng:
+        for q in probs:
+            eng.add(q)
+        eng.evolve(t_ref)
+        t0 = time.perf_counter()
+        obs, st = eng.evolve(t_ref)
+        wall = time.perf_counter() - t0
+        eng.set_option("dense", 0)
+        eng.evolve(t_ref[:2])
+        t1 = time.perf_counter()
+        _, st2 = eng.evolve(t_ref[:k_cheb + 1])
+        wall2 = time.perf_counter() - t1
+    cheb_full = wall2 / k_cheb * (len(t_ref) - 1)
+    return {
+        "workload": "reference default: n_sea=6 (N=7), 13 detunings x 3 variants, t_final 30 s, "
+                    "20000 outputs (sweep_sea_detuning.py:1223-1240)",
+        "engine_mode": st["mode"], "dense_problems": st["dense_problems"],
+        "wall_s": wall, "eig_ms": st["dense_eig_ms"], "dense_ms": st["dense_ms"],
+        "value": len(dets) * 3600.0 / wall, "unit": "detuning-points/hour (measured, whole grid)",
+        "max_norm_error": float(np.max(np.abs(obs[:, 6] - 1.0))),
+        "chebyshev_small_engine": {
+            "intervals_timed": k_cheb, "s_per_interval": wall2 / k_cheb,
+            "full_s_extrapolated": cheb_full, "value": len(dets) * 3600.0 / cheb_full,
+            "max_degree": st2["max_degree"], "launches": st2["step_launches"]},
+        "cpu_reference_note": "ZVODE at the reference tolerances: ~3-16 h per N=7 evolution on one "
+                              "core for this grid (SURVEY.md §6, P2/P5, extrapolated)",
     }
 
 
@@ -313,7 +423,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:  # before any GPU work: the CPU leg forks worker processes
-            cpu = cpu_baseline(args.cpu_budget, args.cpu_cores)
+            cpu = cpu_baseline(args.cpu_fraction, args.cpu_cores)
         except Exception as exc:  # report, never hide
             cpu = {"value": None, "error": repr(exc)}
     import torch
@@ -455,12 +565,22 @@ def main():
     if not args.no_full:
         try:
             line["full_sweep"] = full_sweep(eng, probs, len(my_det) * world, args.full_intervals,
-                                            torch.cuda.synchronize, dist)
+                                            args.full_repeats, torch.cuda.synchronize, dist)
         except Exception as exc:  # report, never hide
             line["full_sweep"] = {"error": repr(exc)}
     if cpu is not None:
         line["cpu_baseline"] = cpu
     eng.close()
+    if rank == 0 and world == 1 and not args.no_config2:
+        try:
+            line["config2"] = config2_leg(local)
+        except Exception as exc:  # report, never hide
+            line["config2"] = {"error": repr(exc)}
+    if rank == 0 and world == 1 and not args.no_refdefault:
+        try:
+            line["reference_default"] = reference_default_leg(local)
+        except Exception as exc:  # report, never hide
+            line["reference_default"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_large:
         try:
             line["large_register"] = large_register(local)

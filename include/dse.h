@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 6
+#define DSE_ABI_VERSION 7
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -87,10 +87,20 @@ typedef struct dse_stats {
   int32_t tile_bits;          /* LDS tile of the first problem (log2 amplitudes per workgroup)  */
   int32_t streams;            /* HIP streams ("lanes") the problems were spread over            */
   int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel, 
-                                 2: streaming with the Walsh-Hadamard engine                     */
+                                 2: streaming with the Walsh-Hadamard engine, 3: every problem on
+                                 the small-register engine, 4: every problem on the dense
+                                 engine (or small and dense)                                     */
   int32_t outputs_per_launch; /* persistent mode: output times per launch (shared series)   */
-  int32_t handoff_fallbacks;  /* evolves of this context re-run on the streaming kernels after  */
-                              /* a cross-tile hand-off timed out (device shared with other work) */
+  int32_t handoff_fallbacks;  /* 1: this call re-ran on the streaming kernels after a          */
+                              /* cross-tile hand-off timed out (device shared with other work)  */
+  int32_t dense_problems;     /* problems this call ran on the dense eigen-propagator engine    */
+                              /* (option "dense")                           */
+  int32_t reserved0;
+  double dense_ms;            /* host wall time of the dense engine (all of its device work)    */
+  double dense_eig_ms;        /* of which the eigendecompositions (rocSOLVER dsyevd)            */
+  double exchange_ms;         /* partitioned registers over processes: time of the exchanges    */
+                              /* (HIP events around each RCCL call on its stream; host wall     */
+                              /* time of each host-transport exchange)                           */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */

@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 6
+DSE_ABI_VERSION = 7
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -57,6 +57,11 @@ class DseStats(C.Structure):
         ("mode", C.c_int32),
         ("outputs_per_launch", C.c_int32),
         ("handoff_fallbacks", C.c_int32),
+        ("dense_problems", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("dense_ms", C.c_double),
+        ("dense_eig_ms", C.c_double),
+        ("exchange_ms", C.c_double),
     ]
 
     def as_dict(self):

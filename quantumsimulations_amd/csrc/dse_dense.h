@@ -1,0 +1,56 @@
+// dse_dense.h -- the dense eigen-propagator engine (dse_dense.hip): SURVEY.md §8(a) K4.
+//
+// For a register of n <= kDenseMaxQubits qubits whose drives are all purely imaginary (drive
+// phase pi/2, the sweep's case) or all real, H is brought to a REAL symmetric form
+//     H' = D H D^dagger,   D |x> = i^{popcount(x)} |x>
+// (a drive flip changes popcount by 1, a double-quantum pair flip by 2: i * (i a) and i^2 g are
+// real), diagonalised once on the device (rocSOLVER dsyevd: H' = V diag(lambda) V^T), and every
+// output is then exact at any time, independent of ||H|| t:
+//     psi'(tau_j) = V (c * exp(-i lambda tau_j)),   c = V^T e_{x0}   (a row of V)
+// Psi' for a block of output times is one real GEMM (rocBLAS dgemm: V times the [cos | -sin]
+// phase columns), the observables are read from its columns (k_dense_obs).  The reference's
+// own default workload (n_sea = 6, 30 s / 20 000 outputs, sweep_sea_detuning.py:1223-1240) needs
+// ~1e8 Chebyshev terms per evolution and one 128 x 128 eigendecomposition this way.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dse {
+
+constexpr int kDenseMaxQubits = 14;  // 2^14 x 2^14 fp64 = 2 GiB per eigenvector matrix
+
+struct DenseProb {
+  int n;              // qubits (engine bit order: bit b = site b)
+  int rot;            // 1: drives imaginary, H' = D H D^dagger; 0: drives real, H' = H
+  uint64_t sea_mask;
+  int rare_bit;       // -1: none in the register
+  int n_sea;          // popcount(sea_mask)
+  uint64_t x0;        // psi(t0) = e_{x0}
+  double shift;       // scalar part of H (a global phase; left out of H')
+  const double* field;  // [n]     sum_b field[b] s_b
+  const double* zz;     // [n * n] sum_{i<j} zz[i n + j] s_i s_j
+  const double* pair;   // [n * n] pair flip coefficient g_ij (i < j), applies iff bit_i == bit_j
+  const double* flip;   // [4 n]   drive flip of bit b: re0 im0 re1 im1 by the output bit value
+  double* V;            // [dim * dim] column-major: H' in, eigenvectors out (rocSOLVER)
+  const double* lam;    // [dim] eigenvalues (ascending)
+  double* obs;          // [n_t][8] raw observable sums of this problem (finish_obs order)
+  double2* final_state; // [dim] psi(t_last) in the reference frame (dse_get_state), or null
+};
+
+// H' of every problem into its (zeroed) V
+hipError_t launch_dense_h(const DenseProb* d, int count, int dim, hipStream_t st);
+// phase columns of output times tau[0 .. tb): P[a + j dim] = c_a cos(lambda_a tau_j),
+// P[a + (tb + j) dim] = -c_a sin(lambda_a tau_j); problem p's block at P + p * pstride
+hipError_t launch_dense_phase(const DenseProb* d, int count, int dim, const double* tau, int tb,
+                              double* P, size_t pstride, hipStream_t st);
+// observables of the tb columns of Psi' (re | im blocks as P) into d[p].obs rows t0 .. t0 + tb
+hipError_t launch_dense_obs(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
+                            int tb, int t0, hipStream_t st);
+// psi(t_last) from column tb - 1 of Psi' into d[p].final_state (frame rotation, psi0 phase and
+// the shift's phase exp(-i shift tau_last) included)
+hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
+                              int tb, double tau_last, hipStream_t st);
+
+}  // namespace dse

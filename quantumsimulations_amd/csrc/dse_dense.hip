@@ -1,0 +1,179 @@
+// dse_dense.hip -- kernels of the dense eigen-propagator engine (dse_dense.h).
+//
+// The eigendecomposition (rocSOLVER dsyevd) and the Psi' = V P product (rocBLAS dgemm, MFMA
+// FP64) are library calls made by the runtime (dse_runtime.hip, dense_run); the kernels here
+// build H' from the coefficient tables, form the phase columns, and reduce the observables.
+#include "dse_dense.h"
+
+namespace dse {
+namespace {
+
+// i^m for m mod 4, as (re, im)
+__device__ __forceinline__ double2 ipow(int m) {
+  m &= 3;
+  return make_double2(m == 0 ? 1.0 : (m == 2 ? -1.0 : 0.0), m == 1 ? 1.0 : (m == 3 ? -1.0 : 0.0));
+}
+
+// Column x of H' (rows y with <y|H'|x> != 0); V is zero on entry.  Matrix elements follow
+// dipolar_ensemble_with_rare.py:453-588 in the bitwise form of SURVEY.md Appendix A.
+__global__ void __launch_bounds__(256)
+k_dense_h(const DenseProb* __restrict__ probs, int dim) {
+  const DenseProb& P = probs[blockIdx.y];
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= (uint32_t)dim) return;
+  const int n = P.n;
+  double* col = P.V + (size_t)x * dim;
+  double d = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double si = 0.5 - (double)((x >> i) & 1u);
+    d += P.field[i] * si;
+    for (int j = i + 1; j < n; ++j) d += P.zz[i * n + j] * si * (0.5 - (double)((x >> j) & 1u));
+  }
+  col[x] = d;
+  const int px = __popc(x);
+  for (int b = 0; b < n; ++b) {
+    const double* f = P.flip + 4 * b;
+    if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
+    const uint32_t y = x ^ (1u << b);
+    const uint32_t vb = (y >> b) & 1u;  // output bit value selects the coefficient
+    const double cr = vb ? f[2] : f[0], ci = vb ? f[3] : f[1];
+    double v = cr;
+    if (P.rot) {  // i^{|y| - |x|} c, real by construction (imaginary drive)
+      const double2 ph = ipow(__popc(y) - px);
+      v = ph.x * cr - ph.y * ci;
+    }
+    col[y] = v;
+  }
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const double g = P.pair[i * n + j];
+      if (g == 0.0 || (((x >> i) ^ (x >> j)) & 1u)) continue;
+      col[x ^ ((1u << i) | (1u << j))] = P.rot ? -g : g;  // i^{+-2} = -1
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_dense_phase(const DenseProb* __restrict__ probs, int dim, const double* __restrict__ tau, int tb,
+              double* __restrict__ Pm, size_t pstride) {
+  const DenseProb& P = probs[blockIdx.z];
+  const uint32_t a = blockIdx.x * 256u + threadIdx.x;
+  const int j = blockIdx.y;
+  if (a >= (uint32_t)dim) return;
+  const double c = P.V[P.x0 + (size_t)a * dim];  // <v_a | e_x0>
+  double s, co;
+  sincos(P.lam[a] * tau[j], &s, &co);
+  double* blk = Pm + blockIdx.z * pstride;
+  blk[a + (size_t)j * dim] = c * co;
+  blk[a + (size_t)(tb + j) * dim] = -c * s;
+}
+
+// block sum of 7 values (256 threads = 4 waves)
+__device__ __forceinline__ void block_sum7(double* v, double (*red)[8]) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) red[w][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) v[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+}
+
+// Same sums as k_obs (dse_kernels.hip): 0 Ix_sea, 1 Iy_sea, 2 Iz_sea, 3 Iz_R, 4 Ix_R, 5 Iy_R,
+// 6 ||psi||^2, with <Ix_k> = sum_{bit_k(x)=0} Re(conj(psi_x) psi_{x^e_k}), <Iy_k> = Im(...).  In the
+// rotated frame psi_x = i^{-|x|} psi'_x, so conj(psi_x) psi_{x^e_k} = -i conj(psi'_x) psi'_{x^e_k}.
+__global__ void __launch_bounds__(256)
+k_dense_obs(const DenseProb* __restrict__ probs, int dim, const double* __restrict__ Psi, size_t pstride,
+            int tb, int t0) {
+  __shared__ double red[4][8];
+  const DenseProb& P = probs[blockIdx.y];
+  const int j = blockIdx.x;
+  const double* re = Psi + blockIdx.y * pstride + (size_t)j * dim;
+  const double* im = re + (size_t)tb * dim;
+  const int n = P.n;
+  const double half_sea = 0.5 * (double)P.n_sea;
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t x = threadIdx.x; x < (uint32_t)dim; x += 256u) {
+    const double ar = re[x], ai = im[x];
+    const double p2 = ar * ar + ai * ai;
+    v[6] += p2;
+    v[2] += p2 * (half_sea - (double)__popcll((uint64_t)x & P.sea_mask));
+    if (P.rare_bit >= 0) v[3] += p2 * (0.5 - (double)((x >> P.rare_bit) & 1u));
+    for (int b = 0; b < n; ++b) {
+      if ((x >> b) & 1u) continue;
+      const bool sea = (P.sea_mask >> b) & 1ull;
+      const bool rr = (b == P.rare_bit);
+      if (!sea && !rr) continue;
+      const uint32_t y = x | (1u << b);
+      const double br = re[y], bi = im[y];
+      double zr = ar * br + ai * bi, zi = ar * bi - ai * br;  // conj(a) b
+      if (P.rot) {  // -i z
+        const double t = zr;
+        zr = zi;
+        zi = -t;
+      }
+      if (sea) v[0] += zr, v[1] += zi;
+      if (rr) v[4] += zr, v[5] += zi;
+    }
+  }
+  block_sum7(v, red);
+  if (threadIdx.x == 0) {
+    double* o = P.obs + (size_t)(t0 + j) * 8;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o[k] = v[k];
+    o[7] = 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+k_dense_final(const DenseProb* __restrict__ probs, int dim, const double* __restrict__ Psi, size_t pstride,
+              int tb, double tau_last) {
+  const DenseProb& P = probs[blockIdx.y];
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= (uint32_t)dim || !P.final_state) return;
+  const double* re = Psi + blockIdx.y * pstride + (size_t)(tb - 1) * dim;
+  const double* im = re + (size_t)tb * dim;
+  // psi_x = exp(-i shift tau) i^{|x0| - |x|} psi'_x   (rot; psi'(0) = e_x0 stands for i^{|x0|} e_x0)
+  double s, c;
+  sincos(-P.shift * tau_last, &s, &c);
+  double2 ph = make_double2(c, s);
+  if (P.rot) {
+    const double2 q = ipow(__popcll(P.x0) - __popc(x));
+    ph = make_double2(ph.x * q.x - ph.y * q.y, ph.x * q.y + ph.y * q.x);
+  }
+  const double ar = re[x], ai = im[x];
+  P.final_state[x] = make_double2(ph.x * ar - ph.y * ai, ph.x * ai + ph.y * ar);
+}
+
+}  // namespace
+
+hipError_t launch_dense_h(const DenseProb* d, int count, int dim, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_h, dim3((dim + 255) / 256, count), dim3(256), 0, st, d, dim);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_phase(const DenseProb* d, int count, int dim, const double* tau, int tb,
+                              double* P, size_t pstride, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_phase, dim3((dim + 255) / 256, tb, count), dim3(256), 0, st, d, dim, tau,
+                     tb, P, pstride);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_obs(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
+                            int tb, int t0, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_obs, dim3(tb, count), dim3(256), 0, st, d, dim, Psi, pstride, tb, t0);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
+                              int tb, double tau_last, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_final, dim3((dim + 255) / 256, count), dim3(256), 0, st, d, dim, Psi,
+                     pstride, tb, tau_last);
+  return hipGetLastError();
+}
+
+}  // namespace dse

@@ -28,9 +28,12 @@
 #include <vector>
 
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include "../../include/dse.h"
 #include "dse_internal.h"
+#include "dse_dense.h"
 #include "dse_small.h"
 #include "dse_wht.h"
 
@@ -70,6 +73,9 @@ struct HostProblem {
   int wht_groups = 0;        // passes' tile-bit groups; 0: this problem uses the step kernels
   // small-register engine (dse_small.hip): n <= 9 qubits, whole evolution one wave per problem
   bool sm = false;           // this evolve runs the problem on that engine
+  // dense eigen-propagator engine (dse_dense.hip): this evolve diagonalises the register instead
+  bool dn = false;
+  bool side() const { return sm || dn; }  // not on the Chebyshev kernels in this evolve
   double2* sm_coef = nullptr;  // into dse_ctx::d_sm_coef
   int* sm_deg = nullptr;
   int final_bsel = 0;        // buffer holding the final state after dse_evolve
@@ -165,6 +171,11 @@ struct dse_ctx {
   void* xuser = nullptr;
   std::vector<unsigned char> xsend, xrecv;
   double xbytes = 0.0;              // bytes this rank sent to other ranks (current evolve)
+  // exchange timing (current evolve): HIP event pairs around RCCL calls (summed at the end of
+  // dse_evolve) plus host wall time of host-transport exchanges
+  std::vector<hipEvent_t> xev;
+  size_t xev_used = 0;
+  double xms = 0.0;
   // small-register engine
   int dbg = 0;                      // diagnostics switches (option "dbg")
   int small = 1;                    // registers of <= 9 qubits run on dse_small.hip
@@ -181,6 +192,11 @@ struct dse_ctx {
   size_t small_out_cap = 0;
   int* d_small_aux = nullptr;       // problem selections per register size, interval -> set map
   size_t small_aux_cap = 0;
+  // dense eigen-propagator engine (dse_dense.h): option "dense" 0 off, 1 when cheaper than the
+  // Chebyshev propagator by the cost model of dense_cheaper (default), 2 for every eligible register
+  int dense = 1;
+  hipStream_t dense_stream = nullptr;
+  rocblas_handle blas = nullptr;
 };
 
 namespace {
@@ -312,6 +328,15 @@ void destroy_lanes(dse_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->small_stream);
     (void)hipStreamDestroy(ctx->small_stream);
     ctx->small_stream = nullptr;
+  }
+  if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas), ctx->blas = nullptr;
+  for (auto e : ctx->xev) (void)hipEventDestroy(e);
+  ctx->xev.clear();
+  ctx->xev_used = 0;
+  if (ctx->dense_stream) {
+    (void)hipStreamSynchronize(ctx->dense_stream);
+    (void)hipStreamDestroy(ctx->dense_stream);
+    ctx->dense_stream = nullptr;
   }
   for (auto& ln : ctx->lanes) {
     if (ln.stream) (void)hipStreamSynchronize(ln.stream);
@@ -742,13 +767,57 @@ int ensure_wht(dse_ctx* ctx) {
 
 // ---- exchanges of a register partitioned over processes: RCCL, or the host transport ----
 // all-to-all of equal chunks (chunk p -> rank p), device buffers
+// Exchange timing: xt_begin/xt_end bracket one exchange on stream st with a HIP event pair
+// (RCCL path; pairs beyond the pool are not timed); xt_sum adds the finished pairs to ctx->xms.
+int xt_begin(dse_ctx* ctx, hipStream_t st, size_t* slot) {
+  *slot = SIZE_MAX;
+  if (ctx->xev_used >= 4096) return DSE_OK;
+  while (ctx->xev.size() < 2 * (ctx->xev_used + 1)) {
+    hipEvent_t e;
+    HIPC(hipEventCreate(&e));
+    ctx->xev.push_back(e);
+  }
+  *slot = ctx->xev_used++;
+  HIPC(hipEventRecord(ctx->xev[2 * *slot], st));
+  return DSE_OK;
+}
+
+int xt_end(dse_ctx* ctx, hipStream_t st, size_t slot) {
+  if (slot != SIZE_MAX) HIPC(hipEventRecord(ctx->xev[2 * slot + 1], st));
+  return DSE_OK;
+}
+
+int xt_sum(dse_ctx* ctx) {
+  for (size_t i = 0; i < ctx->xev_used; ++i) {
+    HIPC(hipEventSynchronize(ctx->xev[2 * i + 1]));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ctx->xev[2 * i], ctx->xev[2 * i + 1]));
+    ctx->xms += ms;
+  }
+  ctx->xev_used = 0;
+  return DSE_OK;
+}
+
+double host_ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int xchg_alltoall(dse_ctx* ctx, const void* src, void* dst, size_t cbytes, hipStream_t st) {
   ctx->xbytes += (double)cbytes * (ctx->dist_world - 1);
   if (!ctx->xfn) {
+    size_t slot;
+    int rc = xt_begin(ctx, st, &slot);
+    if (rc) return rc;
     const ncclResult_t r = ncclAllToAll(src, dst, cbytes, ncclUint8, ctx->comm, st);
     if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclAllToAll: ") + ncclGetErrorString(r));
-    return DSE_OK;
+    return xt_end(ctx, st, slot);
   }
+  const auto h0 = std::chrono::steady_clock::now();
+  struct AddMs {
+    dse_ctx* c;
+    std::chrono::steady_clock::time_point t0;
+    ~AddMs() { c->xms += host_ms_since(t0); }
+  } add_ms{ctx, h0};
   const size_t total = cbytes * ctx->dist_world;
   ctx->xsend.resize(total);
   ctx->xrecv.resize(total);
@@ -907,7 +976,7 @@ int flush_partials(dse_ctx* ctx, size_t nslots, size_t t0, int n_t, double* obs_
   HIPC(hipMemcpy(h.data(), ctx->d_partial, h.size() * sizeof(double), hipMemcpyDeviceToHost));
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     const HostProblem& P = ctx->probs[pi];
-    if (P.sm) continue;  // the small-register engine writes its own sums
+    if (P.side()) continue;  // the small-register engine writes its own sums
     const bool grouped = P.shard_bits > 0 && !P.dist;
     const size_t first_member = grouped ? (size_t)P.group_first : pi;
     const size_t n_members = grouped ? (size_t(1) << P.shard_bits) : 1;
@@ -937,6 +1006,11 @@ int dist_exchange(dse_ctx* ctx, int role, int min_degree, hipStream_t st) {
     if (!P.dist || P.degree < min_degree || !P.xmasks) continue;
     const size_t bytes = (size_t(1) << P.n_local) * sizeof(double2);
     if (ctx->xfn) {  // host transport: one blocking send/recv per partner, masks in ascending order
+      struct AddMs {
+        dse_ctx* c;
+        std::chrono::steady_clock::time_point t0;
+        ~AddMs() { c->xms += host_ms_since(t0); }
+      } add_ms{ctx, std::chrono::steady_clock::now()};
       ctx->xsend.resize(bytes);
       ctx->xrecv.resize(bytes);
       HIPC(hipMemcpyAsync(ctx->xsend.data(), P.buf[role], bytes, hipMemcpyDeviceToHost, st));
@@ -952,6 +1026,9 @@ int dist_exchange(dse_ctx* ctx, int role, int min_degree, hipStream_t st) {
       }
       continue;
     }
+    size_t slot;
+    int rc = xt_begin(ctx, st, &slot);
+    if (rc) return rc;
     if (ncclGroupStart() != ncclSuccess) return fail(ctx, DSE_ERR_HIP, "ncclGroupStart failed");
     for (int m = 1; m < (1 << P.shard_bits); ++m) {
       if (!((P.xmasks >> m) & 1u)) continue;
@@ -966,6 +1043,7 @@ int dist_exchange(dse_ctx* ctx, int role, int min_degree, hipStream_t st) {
     }
     const ncclResult_t r = ncclGroupEnd();
     if (r != ncclSuccess) return fail(ctx, DSE_ERR_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(r));
+    if ((rc = xt_end(ctx, st, slot))) return rc;
   }
   return DSE_OK;
 }
@@ -1110,6 +1188,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     ctx->dbg = (int)value;
   } else if (k == "small") {  // registers of <= 9 qubits on the one-wave engine (dse_small.hip)
     ctx->small = value != 0.0;
+  } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
+    if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "dense must be 0, 1 or 2");
+    ctx->dense = (int)value;
   } else if (k == "small_chunk") {
     if (!(value >= 1 && value <= 1e6)) return fail(ctx, DSE_ERR_ARG, "small_chunk must be in 1..1e6");
     ctx->small_chunk = (int)value;
@@ -1548,6 +1629,176 @@ int small_gather(dse_ctx* ctx, int n_t, double* obs_out) {
   return DSE_OK;
 }
 
+// ---- dense eigen-propagator engine (dse_dense.h) ------------------------------------------
+// A register qualifies when it is whole (not partitioned), holds at most kDenseMaxQubits qubits
+// and its drive coefficients are all purely imaginary (H' = D H D^dagger is real) or all real.
+bool dense_eligible(const HostProblem& P) {
+  if (P.shard_bits != 0 || P.n_local > kDenseMaxQubits) return false;
+  if (P.imag) return true;
+  for (int b = 0; b < P.n; ++b)
+    if (P.flip[4 * b + 1] != 0.0 || P.flip[4 * b + 3] != 0.0) return false;
+  return true;
+}
+
+// Seconds of device time, by the measured rates: the Chebyshev propagator at ~15 TF/s of its
+// algorithmic FP64 work (the N = 14 bench runs at 16.5 chip-level) with ~25 extra terms per
+// output interval, against one eigendecomposition (rocSOLVER dsyevd, ~1e-2 s + 2e-11 s * dim^3)
+// plus the Psi' GEMM at ~40 TF/s and the observable pass.  The long reference grid (30 s, 20 000
+// outputs) goes dense; the 1 ms head-to-head grid at N = 14 stays on Chebyshev.
+bool dense_cheaper(const HostProblem& P, const double* t, int n_t) {
+  if (n_t < 2) return false;
+  const double dim = std::ldexp(1.0, P.n_local);
+  const double alpha = 0.5 * (P.e_max - P.e_min);
+  const double terms = alpha * (t[n_t - 1] - t[0]) + 25.0 * (n_t - 1);
+  const double cheb = terms * dim * (P.flops_per_amp > 0 ? P.flops_per_amp : 300.0) / 15e12;
+  const double dense = 1e-2 + 2e-11 * dim * dim * dim + 4.0 * dim * dim * n_t / 40e12 +
+                       (double)n_t * dim * P.n_local * 32.0 / 2e12;
+  return dense < cheb;
+}
+
+struct DevArena {  // device allocations of one dense_run, freed on every exit path
+  std::vector<void*> ptrs;
+  ~DevArena() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <typename T>
+  T* get(size_t count) {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    return static_cast<T*>(p);
+  }
+};
+
+// Every problem with P.dn: H' built on the device, diagonalised (rocSOLVER dsyevd, batched for
+// registers of equal size), outputs in blocks of TB times as Psi' = V [cos | -sin] (rocBLAS
+// dgemm_strided_batched), observables and the final state from Psi'.  Blocking; writes obs_out.
+int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* ms_all, double* ms_eig) {
+  std::map<int, std::vector<int>> by_n;
+  for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+    if (ctx->probs[pi].dn) by_n[ctx->probs[pi].n_local].push_back((int)pi);
+  if (by_n.empty()) return DSE_OK;
+  const auto c0 = std::chrono::steady_clock::now();
+  double eig_ms = 0.0;
+  if (!ctx->dense_stream) HIPC(hipStreamCreateWithFlags(&ctx->dense_stream, hipStreamNonBlocking));
+  if (!ctx->blas && rocblas_create_handle(&ctx->blas) != rocblas_status_success)
+    return fail(ctx, DSE_ERR_HIP, "rocblas_create_handle failed");
+  hipStream_t st = ctx->dense_stream;
+  if (rocblas_set_stream(ctx->blas, st) != rocblas_status_success)
+    return fail(ctx, DSE_ERR_HIP, "rocblas_set_stream failed");
+  DevArena arena;
+  std::vector<double> tau(n_t);
+  for (int i = 0; i < n_t; ++i) tau[i] = t[i] - t[0];
+  double* d_tau = arena.get<double>(n_t);
+  if (!d_tau) return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed");
+  HIPC(hipMemcpyAsync(d_tau, tau.data(), n_t * sizeof(double), hipMemcpyHostToDevice, st));
+  for (auto& kv : by_n) {
+    const int n = kv.first;
+    const std::vector<int>& list = kv.second;
+    const size_t dim = size_t(1) << n;
+    // outputs per block: P and Psi' of a problem take 2 x dim x 2 TB doubles (<= 256 MiB each)
+    const int TB = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_t, (size_t(256) << 20) / (16 * dim)));
+    const size_t pstride = dim * 2 * (size_t)TB;
+    size_t free_b = 0, total_b = 0;
+    HIPC(hipMemGetInfo(&free_b, &total_b));
+    const size_t per = (dim * dim + 2 * pstride + 3 * dim + (size_t)n_t * 8 + 2 * n * n + 4 * n) * sizeof(double);
+    const size_t B = std::max<size_t>(1, std::min<size_t>(list.size(), (size_t)(0.6 * (double)free_b) / per));
+    for (size_t b0 = 0; b0 < list.size(); b0 += B) {
+      const int cnt = (int)std::min(B, list.size() - b0);
+      DevArena ba;
+      double* V = ba.get<double>(dim * dim * cnt);
+      double* lam = ba.get<double>(dim * cnt);
+      double* E = ba.get<double>(dim * cnt);
+      rocblas_int* info = ba.get<rocblas_int>(cnt);
+      double* Pm = ba.get<double>(pstride * cnt);
+      double* Psi = ba.get<double>(pstride * cnt);
+      double* obs = ba.get<double>((size_t)n_t * 8 * cnt);
+      const size_t tsz = (size_t)(2 * n * n + 5 * n);
+      double* tabs = ba.get<double>(tsz * cnt);
+      DenseProb* d_desc = ba.get<DenseProb>(cnt);
+      if (!V || !lam || !E || !info || !Pm || !Psi || !obs || !tabs || !d_desc)
+        return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed (dim " + std::to_string(dim) + ")");
+      std::vector<double> htabs(tsz * cnt, 0.0);
+      std::vector<DenseProb> desc(cnt);
+      for (int i = 0; i < cnt; ++i) {
+        const HostProblem& P = ctx->probs[list[b0 + i]];
+        double* h = htabs.data() + tsz * i;
+        std::copy(P.field.begin(), P.field.begin() + n, h);
+        std::copy(P.zz.begin(), P.zz.begin() + n * n, h + n);
+        std::copy(P.pair.begin(), P.pair.begin() + n * n, h + n + n * n);
+        std::copy(P.flip.begin(), P.flip.begin() + 4 * n, h + n + 2 * n * n);
+        double* d = tabs + tsz * i;
+        DenseProb& D = desc[i];
+        D.n = n;
+        D.rot = P.imag ? 1 : 0;
+        D.sea_mask = P.sea_mask;
+        D.rare_bit = P.rare_bit;
+        D.n_sea = __builtin_popcountll(P.sea_mask);
+        D.x0 = P.psi0;
+        D.shift = P.shift;
+        D.field = d;
+        D.zz = d + n;
+        D.pair = d + n + n * n;
+        D.flip = d + n + 2 * n * n;
+        D.V = V + dim * dim * i;
+        D.lam = lam + dim * i;
+        D.obs = obs + (size_t)n_t * 8 * i;
+        D.final_state = P.buf[0];
+      }
+      HIPC(hipMemcpyAsync(tabs, htabs.data(), htabs.size() * sizeof(double), hipMemcpyHostToDevice, st));
+      HIPC(hipMemcpyAsync(d_desc, desc.data(), desc.size() * sizeof(DenseProb), hipMemcpyHostToDevice, st));
+      HIPC(hipMemsetAsync(V, 0, dim * dim * cnt * sizeof(double), st));
+      HIPC(launch_dense_h(d_desc, cnt, (int)dim, st));
+      HIPC(hipStreamSynchronize(st));
+      const auto e0 = std::chrono::steady_clock::now();
+      rocblas_status rs;
+      if (cnt == 1)
+        rs = rocsolver_dsyevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, (rocblas_int)dim, V,
+                              (rocblas_int)dim, lam, E, info);
+      else
+        rs = rocsolver_dsyevd_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper,
+                                              (rocblas_int)dim, V, (rocblas_int)dim, (rocblas_stride)(dim * dim),
+                                              lam, (rocblas_stride)dim, E, (rocblas_stride)dim, info, cnt);
+      if (rs != rocblas_status_success)
+        return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)rs) + ")");
+      std::vector<rocblas_int> hinfo(cnt);
+      HIPC(hipMemcpyAsync(hinfo.data(), info, cnt * sizeof(rocblas_int), hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+      eig_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e0).count();
+      for (int i = 0; i < cnt; ++i)
+        if (hinfo[i] != 0)
+          return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: dsyevd did not converge (info " +
+                                                    std::to_string(hinfo[i]) + ")");
+      const double one = 1.0, zero = 0.0;
+      for (int tb0 = 0; tb0 < n_t; tb0 += TB) {
+        const int tb = std::min(TB, n_t - tb0);
+        HIPC(launch_dense_phase(d_desc, cnt, (int)dim, d_tau + tb0, tb, Pm, pstride, st));
+        rs = rocblas_dgemm_strided_batched(ctx->blas, rocblas_operation_none, rocblas_operation_none,
+                                           (rocblas_int)dim, 2 * tb, (rocblas_int)dim, &one, V, (rocblas_int)dim,
+                                           (rocblas_stride)(dim * dim), Pm, (rocblas_int)dim,
+                                           (rocblas_stride)pstride, &zero, Psi, (rocblas_int)dim,
+                                           (rocblas_stride)pstride, cnt);
+        if (rs != rocblas_status_success)
+          return fail(ctx, DSE_ERR_HIP, "rocblas dgemm failed (status " + std::to_string((int)rs) + ")");
+        HIPC(launch_dense_obs(d_desc, cnt, (int)dim, Psi, pstride, tb, tb0, st));
+        if (tb0 + tb == n_t) HIPC(launch_dense_final(d_desc, cnt, (int)dim, Psi, pstride, tb, tau[n_t - 1], st));
+      }
+      std::vector<double> h((size_t)n_t * 8 * cnt);
+      HIPC(hipMemcpyAsync(h.data(), obs, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+      for (int i = 0; i < cnt; ++i) {
+        const int pi = list[b0 + i];
+        for (int ti = 0; ti < n_t; ++ti)
+          finish_obs(ctx->probs[pi], h.data() + ((size_t)i * n_t + ti) * 8,
+                     obs_out + (size_t)pi * DSE_N_OBS * n_t + ti, (size_t)n_t);
+      }
+    }
+  }
+  if (ms_all) *ms_all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+  if (ms_eig) *ms_eig = eig_ms;
+  return DSE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1639,6 +1890,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   int rc = prepare(ctx);
   if (rc) return rc;
   ctx->xbytes = 0.0;
+  ctx->xms = 0.0;
+  ctx->xev_used = 0;
 
   phase("prepare");
   // ---- execution mode ----
@@ -1646,16 +1899,21 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // other problems run on.  Of the rest -- persistent: every problem fits one or two
   // register-block tiles -> one k_interval launch per group of output intervals and lane;
   // streaming: per-term kernels, one output per group.
-  bool any_small = false, any_big = false;
+  // dense engine first (option "dense"): a register it takes is off every Chebyshev path
+  bool any_small = false, any_big = false, any_dense = false;
   for (auto& P : ctx->probs) {
-    P.sm = ctx->small && P.shard_bits == 0 && P.n_local <= kSmallMaxQubits;
+    P.dn = ctx->dense && dense_eligible(P) && (ctx->dense == 2 || dense_cheaper(P, t, n_t));
+    any_dense = any_dense || P.dn;
+  }
+  for (auto& P : ctx->probs) {
+    P.sm = !P.dn && ctx->small && P.shard_bits == 0 && P.n_local <= kSmallMaxQubits;
     any_small = any_small || P.sm;
-    any_big = any_big || !P.sm;
+    any_big = any_big || !P.side();
   }
   bool persistent = ctx->persistent != 0;
   bool any_dist = false;
   for (auto& P : ctx->probs) {
-    if (P.sm) continue;
+    if (P.side()) continue;
     if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
     any_dist = any_dist || P.dist;
   }
@@ -1678,7 +1936,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   double max_z = 0.0;
   for (int m = 0; m + 1 < n_t; ++m)
     for (auto& P : ctx->probs)
-      if (!P.sm) max_z = std::max(max_z, 0.5 * (P.e_max - P.e_min) * (t[m + 1] - t[m]));
+      if (!P.side()) max_z = std::max(max_z, 0.5 * (P.e_max - P.e_min) * (t[m + 1] - t[m]));
   int M = 1;
   if (persistent && max_z < 400.0) M = std::max(1, std::min(ctx->outputs_per_launch, n_t - 1));
 
@@ -1721,7 +1979,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   std::vector<std::string> coef_msg(ctx->probs.size());
   auto coef_one = [&](size_t pi) {
     HostProblem& P = ctx->probs[pi];
-    if (P.sm) return;
+    if (P.side()) return;
     const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
     const double beta = 0.5 * (P.e_max + P.e_min);
     int deg = 1;
@@ -1788,7 +2046,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   }
   coef_arena.host.reserve(coef_total);
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
-    if (!ctx->probs[pi].sm) coef_off[pi] = coef_arena.place(coef_rows[pi].size() * sizeof(double2));
+    if (!ctx->probs[pi].side()) coef_off[pi] = coef_arena.place(coef_rows[pi].size() * sizeof(double2));
   parallel_for(ctx->probs.size(), [&](size_t pi) {
     if (!coef_rows[pi].empty())
       std::memcpy(coef_arena.host.data() + coef_off[pi], coef_rows[pi].data(), coef_rows[pi].size() * sizeof(double2));
@@ -1798,7 +2056,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   if ((rc = upload_arena(ctx, coef_arena, &ctx->d_coef, &ctx->coef_cap, ctx->lanes[0].stream))) return rc;
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
     HostProblem& P = ctx->probs[pi];
-    if (P.sm) continue;
+    if (P.side()) continue;
     P.coef = reinterpret_cast<double2*>(ctx->d_coef + coef_off[pi]);
     ctx->h_desc[pi].coef = P.coef;
   }
@@ -1812,7 +2070,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     size_t need = 0;
     if (M > 1)
       for (auto& P : ctx->probs)
-        if (!P.sm) need += xsets * ((size_t)(M - 1) << P.n_local);
+        if (!P.side()) need += xsets * ((size_t)(M - 1) << P.n_local);
     if (need > ctx->xacc_cap) {
       if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
       ctx->xacc_cap = 0;
@@ -1823,7 +2081,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     }
     size_t off = 0;
     for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
-      const bool use = M > 1 && !ctx->probs[pi].sm;
+      const bool use = M > 1 && !ctx->probs[pi].side();
       ctx->h_desc[pi].xacc = use ? ctx->d_xacc + off : nullptr;
       if (use) off += xsets * ((size_t)(M - 1) << ctx->probs[pi].n_local);
     }
@@ -1856,10 +2114,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
   // dist shards: one lane, so the RCCL exchanges are stream-ordered with every launch
   int n_big = 0;
-  for (auto& P : ctx->probs) n_big += P.sm ? 0 : 1;
+  for (auto& P : ctx->probs) n_big += P.side() ? 0 : 1;
   const int n_lanes = any_dist ? 1 : std::max(1, std::min<int>(ctx->n_streams, n_big));
   bool imag_all = true;
-  for (auto& P : ctx->probs) imag_all = imag_all && (P.sm || P.imag);
+  for (auto& P : ctx->probs) imag_all = imag_all && (P.side() || P.imag);
   // 2-tile interval launches go out in chunks whose workgroups can all be resident at once (the
   // pairs hand off every term): the occupancy query x compute units, even.
   int64_t pair_cap = 2;
@@ -1882,17 +2140,17 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // pair whose partner is still queued waits only for a workgroup that needs no partner.
   std::map<int, std::pair<int64_t, int64_t>> tiles_per_L;  // L -> (1-tile problems, 2-tile problems)
   for (auto& P : ctx->probs)
-    if (!P.sm && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
+    if (!P.side() && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
       (P.n_tiles == 1 ? tiles_per_L[P.L].first : tiles_per_L[P.L].second) += 1;
   auto mixed_L = [&](const HostProblem& P) {
-    if (!persistent || !ctx->mixed_launch || P.sm || P.shard_bits != 0 || P.n_tiles > 2) return false;
+    if (!persistent || !ctx->mixed_launch || P.side() || P.shard_bits != 0 || P.n_tiles > 2) return false;
     const auto it = tiles_per_L.find(P.L);
     return it != tiles_per_L.end() && it->second.first > 0 && it->second.second > 0 &&
            2 * it->second.second <= cap;
   };
   std::vector<int> order;
   for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
-    if (!ctx->probs[pi].sm) order.push_back((int)pi);
+    if (!ctx->probs[pi].side()) order.push_back((int)pi);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
     return ctx->probs[a].degree > ctx->probs[b].degree;
   });
@@ -2070,6 +2328,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   double small_happl = 0.0, small_launches = 0.0;
   if (any_small && (rc = small_launch(ctx, t, n_t, tol, &small_happl, &small_launches))) return rc;
 
+  double dense_ms = 0.0, dense_eig_ms = 0.0;
+  if (any_dense && (rc = dense_run(ctx, t, n_t, obs_out, &dense_ms, &dense_eig_ms))) return rc;
   phase("psi0/small");
   const size_t chunk = (size_t)std::max<int64_t>(M, std::min<int64_t>(
       n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64))));
@@ -2270,13 +2530,13 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   }
   phase("tail");
   ctx->last_q = n_groups & 1;
-  for (auto& P : ctx->probs) P.final_bsel = P.sm ? 0 : (ctx->last_q ? 2 : 0);
+  for (auto& P : ctx->probs) P.final_bsel = P.side() ? 0 : (ctx->last_q ? 2 : 0);
   ctx->evolved = true;
 
   if (stats) {
     double happl = small_happl;
     for (auto& P : ctx->probs)
-      if (!P.sm) happl += (double)P.degree * n_groups;
+      if (!P.side()) happl += (double)P.degree * n_groups;
     std::memset(stats, 0, sizeof(*stats));
     stats->h_applications = happl;
     stats->amplitude_updates = amp_updates;
@@ -2284,7 +2544,12 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->h_flops = all_flops;
     stats->timed_flops = flops_timed;
     stats->timed_amp_terms = amps_timed;
-    stats->mode = !any_big ? 3 : (persistent ? 1 : (used_wht ? 2 : 0));
+    stats->mode = !any_big ? (any_dense ? 4 : 3) : (persistent ? 1 : (used_wht ? 2 : 0));
+    int n_dense = 0;
+    for (auto& P : ctx->probs) n_dense += P.dn ? 1 : 0;
+    stats->dense_problems = n_dense;
+    stats->dense_ms = dense_ms;
+    stats->dense_eig_ms = dense_eig_ms;
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
     stats->step_launches = launches + small_launches;
     stats->timed_launches = launches_timed;
@@ -2299,6 +2564,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->outputs_per_launch = M;
     stats->handoff_fallbacks = ctx->handoff_fallbacks;
     stats->exchange_bytes = ctx->xbytes;
+    if ((rc = xt_sum(ctx))) return rc;
+    stats->exchange_ms = ctx->xms;
   }
   return DSE_OK;
 }

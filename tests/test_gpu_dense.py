@@ -1,0 +1,109 @@
+"""The dense eigen-propagator engine (csrc/dse_dense.{h,hip}): H' = D H D^dagger
+made real (D|x> = i^popcount(x) |x>), diagonalised once on the device (rocSOLVER dsyevd), every
+output time exact from one GEMM (rocBLAS dgemm) and the observable pass.
+
+* N = 7, 3 variants, 2 ms / 201 outputs, against the exact-eigh fixture of the reference-built H
+  (1e-10) and against the Chebyshev engines (1e-11)
+* N = 12 center_on (config 2) against its exact-eigh fixture (1e-10)
+* the final state (dse_get_state: frame rotation, psi0 phase, shift phase) equals the Chebyshev
+  engine's, and a grid past one output block (TB) stays consistent
+* the reference's default workload (n_sea = 6, 13 detunings x 3 variants, 30 s / 20 000 outputs,
+  sweep_sea_detuning.py:1223-1240) goes to the dense engine by the cost model (option dense = 1)
+  and its first outputs agree with the Chebyshev engine on the same grid prefix; its norms stay 1
+* the cost model keeps the 1 ms N = 14 grid on the Chebyshev kernels
+"""
+import numpy as np
+import pytest
+
+from oracle import reference_model as rm
+from quantumsimulations_amd import problem as pb
+from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
+
+pytestmark = pytest.mark.gpu
+OBS = rm.OBS_ORDER
+
+
+def _evolve(engine, params, t, dense):
+    engine.clear()
+    engine.set_option("dense", dense)
+    try:
+        for p in params:
+            engine.add(pb.build_problem(p))
+        obs, st = engine.evolve(t)
+        states = [engine.state(i) for i in range(len(params))]
+    finally:
+        engine.set_option("dense", 1)
+    engine.clear()
+    return obs, st, states
+
+
+def test_dense_matches_exact_and_chebyshev_n7(engine, golden):
+    tr = golden("traces_n7.npz")
+    t = tr["t"]
+    params = [sweep_point_params(6, 50000.0, v, 2e-3, 201) for v in VARIANTS]
+    dn, st, s_dn = _evolve(engine, params, t, 2)
+    assert st["dense_problems"] == 3 and st["mode"] == 4
+    ch, st2, s_ch = _evolve(engine, params, t, 0)
+    assert st2["dense_problems"] == 0
+    for i, v in enumerate(VARIANTS):
+        for j, k in enumerate(OBS):
+            err = np.max(np.abs(dn[i, j] - tr[f"{v}_exact_{k}"]))
+            assert err < 1e-10, (v, k, err)
+    np.testing.assert_allclose(dn, ch, rtol=0, atol=1e-11)
+    for a, b in zip(s_dn, s_ch):
+        assert np.max(np.abs(a - b)) < 1e-11
+
+
+def test_dense_config2_n12_matches_exact(engine, golden):
+    tr = golden("traces_n12.npz")
+    t = tr["t"]
+    p = sweep_point_params(11, 50000.0, "center_on", float(t[-1]), len(t))
+    dn, st, _ = _evolve(engine, [p], t, 2)
+    assert st["dense_problems"] == 1
+    for j, k in enumerate(OBS):
+        err = np.max(np.abs(dn[0, j] - tr[f"exact_{k}"]))
+        assert err < 1e-10, (k, err)
+
+
+def test_dense_long_grid_blocks_and_final_state(engine):
+    # 3000 outputs over 30 ms: the Chebyshev engines take ~1e5 terms; the dense engine one
+    # eigendecomposition.  Same traces and final state.
+    t = np.linspace(0.0, 3e-2, 3000)
+    params = [sweep_point_params(6, d, v, 3e-2, 3000) for d in (0.0, 150e3) for v in VARIANTS]
+    dn, st, s_dn = _evolve(engine, params, t, 2)
+    ch, _, s_ch = _evolve(engine, params, t, 0)
+    assert st["dense_problems"] == len(params)
+    assert np.max(np.abs(dn - ch)) < 1e-9
+    for a, b in zip(s_dn, s_ch):
+        assert np.max(np.abs(a - b)) < 1e-9
+
+
+def test_reference_default_workload_goes_dense(engine):
+    t_ref = np.linspace(0.0, 30.0, 20000)
+    dets = np.linspace(0.0, 150e3, 13)
+    params = [sweep_point_params(6, float(d), v, 30.0, 20000) for d in dets for v in VARIANTS]
+    engine.clear()
+    for p in params:
+        engine.add(pb.build_problem(p))
+    obs, st = engine.evolve(t_ref)
+    engine.clear()
+    assert st["dense_problems"] == len(params) and st["mode"] == 4
+    np.testing.assert_allclose(obs[:, 6], 1.0, atol=1e-10)
+    # the first 12 intervals on the small-register Chebyshev engine (reference grid prefix)
+    K = 12
+    for p in params:
+        engine.add(pb.build_problem(p))
+    ch, st2 = engine.evolve(t_ref[:K + 1])
+    engine.clear()
+    assert st2["dense_problems"] == 0
+    assert np.max(np.abs(obs[:, :, :K + 1] - ch)) < 1e-10
+
+
+def test_cost_model_keeps_short_n14_grid_on_chebyshev(engine):
+    t = np.linspace(0.0, 1e-3, 101)
+    engine.clear()
+    for v in VARIANTS:
+        engine.add(pb.build_problem(sweep_point_params(13, 75e3, v, 1e-3, 101)))
+    _, st = engine.evolve(t)
+    engine.clear()
+    assert st["dense_problems"] == 0 and st["mode"] == 1

@@ -121,6 +121,11 @@ def main():
             # the exchange's bytes per link over the whole call's wall time: a lower bound of the
             # per-link rate while the exchange runs (the passes run between exchanges)
             "xgmi_gbs_per_link_lower_bound": (measured / links / wall / 1e9) if not a.loopback else None,
+            # the same bytes over the time the exchanges themselves took (HIP events around each
+            # RCCL call on its stream; host wall time for the host transport)
+            "exchange_ms": st.get("exchange_ms"),
+            "xgmi_gbs_per_link": (measured / links / (st["exchange_ms"] * 1e-3) / 1e9)
+            if (not a.loopback and st.get("exchange_ms")) else None,
             "obs_t_final": obs_d,
             # exact propagation conserves the norm: the end-to-end check of the exchanged path
             "norm_error": abs(obs_d["state_norm"] - 1.0),
