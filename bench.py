@@ -101,7 +101,8 @@ def parse():
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command (tools/gpu_profile.sh +
 # tools/pmc_summary.py), newest round first
 PMC_TRAFFIC = [os.path.join(ROOT, "profiles", r, f) for r, f in
-               (("r02", "bench_pmc_traffic.json"), ("r01", "v9_pmc_traffic.json"))]
+               (("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
+                ("r01", "v9_pmc_traffic.json"))]
 
 
 def pmc_traffic(kernel: str):
@@ -206,7 +207,8 @@ def large_register(device: int, n_sea: int = 29):
     }
 
 
-def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, dist=None):
+def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, dist=None,
+               dense_points=(0.0, 150e3)):
     """The reference's grid (sweep_sea_detuning.py:1223-1224: t_final 30 s, 20000 outputs ->
     dt = 1.5 ms, alpha dt ~ 3e3..1e4: one output per launch, ~1e4 Chebyshev terms each) on the
     bench's evolutions: one interval untimed (coefficients, warm-up), then `repeats` timed runs of
@@ -225,7 +227,7 @@ def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, di
     h_per_ev = st["h_applications"] / len(probs) / intervals     # H applications per evolution
     k_ms = st["step_kernel_ms"]
     gbs = 80.0 * st["timed_amp_terms"] / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
-    return {
+    cheb = {
         "grid": "t_final 30 s, 20000 outputs (sweep_sea_detuning.py:1223-1224)",
         "intervals_timed": intervals, "repeats": len(per), "s_per_interval": per_interval,
         "s_per_interval_min": float(np.min(per)), "s_per_interval_max": float(np.max(per)),
@@ -238,9 +240,59 @@ def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, di
         "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(st["mode"], "streaming"),
         "kernel_gbs_80B_per_amp_term": gbs,
         "kernel_frac_hbm": gbs / HBM_PEAK_GBS if gbs else None,
-        "note": "the BASELINE '(full sweep)' figure: this grid, extrapolated from the timed intervals "
-                "(headline `value` is the 1 ms head-to-head grid); the reference's own ZVODE trace of "
-                "this grid takes ~430-1530 h per N=14 evolution on one core (SURVEY.md §6)",
+    }
+    out = {"grid": cheb["grid"], "chebyshev": cheb}
+    dense = None
+    if dense_points:
+        try:
+            dense = full_sweep_dense(eng.device, dense_points, sync, dist)
+        except Exception as exc:  # report, never hide
+            dense = {"error": repr(exc)}
+        out["dense"] = dense
+    best = cheb
+    if dense and dense.get("full_sweep_s_extrapolated") and dense["full_sweep_s_extrapolated"] < full_s:
+        best = dense
+    out.update({
+        "engine": "dense eigen-propagator" if best is dense else "chebyshev",
+        "full_sweep_s_extrapolated": best["full_sweep_s_extrapolated"],
+        "value": n_points * 3600.0 / best["full_sweep_s_extrapolated"],
+        "unit": "detuning-points/hour (extrapolated)",
+        "note": "BASELINE's '(full sweep)' figure: the reference grid on the bench's 64 x 3 evolutions, by "
+                "the engine libdse's cost model picks for that grid (option dense = 1: the dense "
+                "eigen-propagator, whose cost per evolution does not depend on the detuning, timed whole "
+                "on sample points and scaled to 64; the Chebyshev engines timed on 16-interval runs and "
+                "scaled to 19999 intervals); headline `value` is the 1 ms head-to-head grid; the "
+                "reference's own ZVODE trace of this grid takes ~430-1530 h per N=14 evolution on one "
+                "core (SURVEY.md §6)",
+    })
+    return out
+
+
+def full_sweep_dense(device: int, dets, sync, dist=None):
+    """The dense eigen-propagator on the WHOLE reference grid (20000 outputs) for the 3 variants of
+    the sample detunings, one evolve per detuning (timed whole, barrier + sync around): its work per
+    evolution is one eigendecomposition + the output GEMMs, independent of the detuning, so the
+    sweep's cost = 64 x the mean per-point time (the sample's spread reported)."""
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.engine import Engine
+    from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
+    t_ref = np.linspace(0.0, 30.0, 20000)
+    per_point, stats = [], []
+    with Engine(device) as eng:
+        for d in dets:
+            eng.clear()
+            for v in VARIANTS:
+                eng.add(pb.build_problem(sweep_point_params(N_SEA, float(d), v, 30.0, 20000)))
+            dt = timed_steps(lambda: stats.append(eng.evolve(t_ref)[1]), 1, 0, sync, dist)
+            per_point.append(dt)
+    st = stats[-1]
+    mean = float(np.mean(per_point))
+    return {
+        "sample_detunings_hz": [float(d) for d in dets], "s_per_point": per_point,
+        "s_per_point_mean": mean, "dense_problems": st["dense_problems"],
+        "eig_ms_last_point": st["dense_eig_ms"], "dense_ms_last_point": st["dense_ms"],
+        "full_sweep_s_extrapolated": mean * N_DET,
+        "value": N_DET * 3600.0 / (mean * N_DET),
     }
 
 

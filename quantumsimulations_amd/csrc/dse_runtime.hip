@@ -1642,17 +1642,19 @@ bool dense_eligible(const HostProblem& P) {
 
 // Seconds of device time, by the measured rates: the Chebyshev propagator at ~15 TF/s of its
 // algorithmic FP64 work (the N = 14 bench runs at 16.5 chip-level) with ~25 extra terms per
-// output interval, against one eigendecomposition (rocSOLVER dsyevd, ~1e-2 s + 2e-11 s * dim^3)
-// plus the Psi' GEMM at ~40 TF/s and the observable pass.  The long reference grid (30 s, 20 000
-// outputs) goes dense; the 1 ms head-to-head grid at N = 14 stays on Chebyshev.
+// output interval, against one eigendecomposition (dsyevd on MI355X, profiles/r03/probe.jsonl:
+// 0.15 / 0.68 / 4.1 s at dim 4096 / 8192 / 16384, 3 ms for 39 registers of dim 128 together:
+// 6.4e-13 dim^3 + 4.9e-9 dim^2, + 20 ms from dim 1024 up) plus the Psi' GEMM at ~40 TF/s and the
+// observable pass.  The long reference grid (30 s, 20 000 outputs) goes dense at every register
+// size; the 1 ms head-to-head grid at N = 14 and config 2 (N = 12, 2 ms) stay on Chebyshev.
 bool dense_cheaper(const HostProblem& P, const double* t, int n_t) {
   if (n_t < 2) return false;
   const double dim = std::ldexp(1.0, P.n_local);
   const double alpha = 0.5 * (P.e_max - P.e_min);
   const double terms = alpha * (t[n_t - 1] - t[0]) + 25.0 * (n_t - 1);
   const double cheb = terms * dim * (P.flops_per_amp > 0 ? P.flops_per_amp : 300.0) / 15e12;
-  const double dense = 1e-2 + 2e-11 * dim * dim * dim + 4.0 * dim * dim * n_t / 40e12 +
-                       (double)n_t * dim * P.n_local * 32.0 / 2e12;
+  const double eig = 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
+  const double dense = eig + 4.0 * dim * dim * n_t / 40e12 + (double)n_t * dim * P.n_local * 32.0 / 2e12;
   return dense < cheb;
 }
 
@@ -1751,14 +1753,16 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       HIPC(launch_dense_h(d_desc, cnt, (int)dim, st));
       HIPC(hipStreamSynchronize(st));
       const auto e0 = std::chrono::steady_clock::now();
-      rocblas_status rs;
-      if (cnt == 1)
-        rs = rocsolver_dsyevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, (rocblas_int)dim, V,
-                              (rocblas_int)dim, lam, E, info);
-      else
+      rocblas_status rs = rocblas_status_success;
+      if (dim >= 1024) {  // large registers one by one (the batched solver targets small matrices)
+        for (int i = 0; i < cnt && rs == rocblas_status_success; ++i)
+          rs = rocsolver_dsyevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, (rocblas_int)dim,
+                                V + dim * dim * i, (rocblas_int)dim, lam + dim * i, E + dim * i, info + i);
+      } else {
         rs = rocsolver_dsyevd_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper,
                                               (rocblas_int)dim, V, (rocblas_int)dim, (rocblas_stride)(dim * dim),
                                               lam, (rocblas_stride)dim, E, (rocblas_stride)dim, info, cnt);
+      }
       if (rs != rocblas_status_success)
         return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)rs) + ")");
       std::vector<rocblas_int> hinfo(cnt);
