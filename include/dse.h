@@ -89,7 +89,9 @@ typedef struct dse_stats {
   int32_t mode;               /* 0: per-term streaming kernels, 1: persistent interval kernel, 
                                  2: streaming with the Walsh-Hadamard engine, 3: every problem on
                                  the small-register engine, 4: every problem on the dense
-                                 engine (or small and dense)                                     */
+                                 engine (or small and dense), 5: the context's register in
+                                 propagator-matrix mode (U = exp(-iH dt) built column-parallel,
+                                 outputs by repeated products; option "matrix")                 */
   int32_t outputs_per_launch; /* persistent mode: output times per launch (shared series)   */
   int32_t handoff_fallbacks;  /* 1: this call re-ran on the streaming kernels after a          */
                               /* cross-tile hand-off timed out (device shared with other work)  */

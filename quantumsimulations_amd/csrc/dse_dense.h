@@ -48,6 +48,10 @@ hipError_t launch_dense_phase(const DenseProb* d, int count, int dim, const doub
 // observables of the tb columns of Psi' (re | im blocks as P) into d[p].obs rows t0 .. t0 + tb
 hipError_t launch_dense_obs(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
                             int tb, int t0, hipStream_t st);
+// observables of n_states complex states (dim amplitudes each, consecutive) of one problem
+// (d->rot = 0: the computational frame) into d->obs rows t0 .. t0 + n_states
+hipError_t launch_state_obs(const DenseProb* d, int dim, const double2* states, int n_states, int t0,
+                            hipStream_t st);
 // psi(t_last) from column tb - 1 of Psi' into d[p].final_state (frame rotation, psi0 phase and
 // the shift's phase exp(-i shift tau_last) included)
 hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,

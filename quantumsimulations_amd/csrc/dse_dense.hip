@@ -86,19 +86,22 @@ __device__ __forceinline__ void block_sum7(double* v, double (*red)[8]) {
 // Same sums as k_obs (dse_kernels.hip): 0 Ix_sea, 1 Iy_sea, 2 Iz_sea, 3 Iz_R, 4 Ix_R, 5 Iy_R,
 // 6 ||psi||^2, with <Ix_k> = sum_{bit_k(x)=0} Re(conj(psi_x) psi_{x^e_k}), <Iy_k> = Im(...).  In the
 // rotated frame psi_x = i^{-|x|} psi'_x, so conj(psi_x) psi_{x^e_k} = -i conj(psi'_x) psi'_{x^e_k}.
+// Columns j of Psi' at Psi + p pstride + j colstride (real parts), imaginary parts imoff further,
+// elements es doubles apart: the dense engine's [re | im] blocks (colstride dim, imoff tb dim,
+// es 1) or interleaved complex states (colstride 2 dim, imoff 1, es 2).
 __global__ void __launch_bounds__(256)
 k_dense_obs(const DenseProb* __restrict__ probs, int dim, const double* __restrict__ Psi, size_t pstride,
-            int tb, int t0) {
+            size_t colstride, size_t imoff, int es, int t0) {
   __shared__ double red[4][8];
   const DenseProb& P = probs[blockIdx.y];
   const int j = blockIdx.x;
-  const double* re = Psi + blockIdx.y * pstride + (size_t)j * dim;
-  const double* im = re + (size_t)tb * dim;
+  const double* re = Psi + blockIdx.y * pstride + (size_t)j * colstride;
+  const double* im = re + imoff;
   const int n = P.n;
   const double half_sea = 0.5 * (double)P.n_sea;
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   for (uint32_t x = threadIdx.x; x < (uint32_t)dim; x += 256u) {
-    const double ar = re[x], ai = im[x];
+    const double ar = re[(size_t)x * es], ai = im[(size_t)x * es];
     const double p2 = ar * ar + ai * ai;
     v[6] += p2;
     v[2] += p2 * (half_sea - (double)__popcll((uint64_t)x & P.sea_mask));
@@ -109,7 +112,7 @@ k_dense_obs(const DenseProb* __restrict__ probs, int dim, const double* __restri
       const bool rr = (b == P.rare_bit);
       if (!sea && !rr) continue;
       const uint32_t y = x | (1u << b);
-      const double br = re[y], bi = im[y];
+      const double br = re[(size_t)y * es], bi = im[(size_t)y * es];
       double zr = ar * br + ai * bi, zi = ar * bi - ai * br;  // conj(a) b
       if (P.rot) {  // -i z
         const double t = zr;
@@ -165,7 +168,15 @@ hipError_t launch_dense_phase(const DenseProb* d, int count, int dim, const doub
 
 hipError_t launch_dense_obs(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
                             int tb, int t0, hipStream_t st) {
-  hipLaunchKernelGGL(k_dense_obs, dim3(tb, count), dim3(256), 0, st, d, dim, Psi, pstride, tb, t0);
+  hipLaunchKernelGGL(k_dense_obs, dim3(tb, count), dim3(256), 0, st, d, dim, Psi, pstride, (size_t)dim,
+                     (size_t)tb * dim, 1, t0);
+  return hipGetLastError();
+}
+
+hipError_t launch_state_obs(const DenseProb* d, int dim, const double2* states, int n_states, int t0,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_obs, dim3(n_states, 1), dim3(256), 0, st, d, dim, (const double*)states,
+                     (size_t)0, (size_t)2 * dim, (size_t)1, 2, t0);
   return hipGetLastError();
 }
 

@@ -156,8 +156,10 @@ bool interval_supported(int L);
 // resident workgroups of k_interval<L> per compute unit (occupancy query)
 hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu);
 // imag: every drive coefficient of the launched problems is purely imaginary (HostProblem::imag)
+// colstride > 0: column mode (one-tile register, item.y = column, buffers offset by column *
+// colstride amplitudes): every column propagated over the interval of coefficient set `set`
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items, int q,
-                           int set, int n_out, int* flags, int* err, hipStream_t st);
+                           int set, int n_out, int* flags, int* err, hipStream_t st, long colstride = 0);
 // zeroes the interval kernel's hand-off flags of the given items (before a 2-tile launch)
 hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st);
 // psi(t0) of many registers in one launch: entry i zeroes ptr[0 .. n) and sets ptr[one_at] = 1

@@ -144,7 +144,7 @@ struct IvShared {
 template <int L, bool IMAG>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
-           int n_out, int* __restrict__ flags, int* __restrict__ err) {
+           int n_out, int* __restrict__ flags, int* __restrict__ err, long colstride) {
   constexpr int NT = RB<L>::NT, R = kRegAmps, TB = RB<L>::TB, NH = R / 2;
   // software-pipelined partner reads in the fused loop (the production IMAG build; the general
   // build keeps the plain order, which fits its larger drive arithmetic without spilling)
@@ -158,7 +158,10 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
-  const uint32_t h = (uint32_t)it.y;
+  // column mode (colstride > 0, the propagator-matrix build of dse_runtime's matrix_run): a
+  // one-tile register, item.y = the column; its state buffers start column * colstride in
+  const uint32_t h = colstride ? 0u : (uint32_t)it.y;
+  const size_t coff = colstride ? (size_t)it.y * (size_t)colstride : 0;
   const int tid = threadIdx.x;
   const bool pair = (P.n == L + 1);
   const bool xgen = pair && P.n_pairs_hi > 0;  // pairs cross the tile boundary: u pre-pass
@@ -171,11 +174,11 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   // P.xslots[(tile * kXSlots + (k - 1) % kXSlots) << L] carries the operand of term k.  The
   // partner's w_0 is read from its psi tile.
   constexpr uint32_t TBYTES = T * 16u;
-  const __amdgpu_buffer_rsrc_t psi_me = tile_rsrc(P.buf[q ? 2 : 0] + (h << L), TBYTES);
+  const __amdgpu_buffer_rsrc_t psi_me = tile_rsrc(P.buf[q ? 2 : 0] + coff + (h << L), TBYTES);
   const __amdgpu_buffer_rsrc_t psi_pa = tile_rsrc(P.buf[q ? 2 : 0] + ((h ^ 1u) << L), TBYTES);
   double2* const xs_me = P.xslots + ((size_t)h * kXSlots << L);
   double2* const xs_pa = P.xslots + ((size_t)(h ^ 1u) * kXSlots << L);
-  const __amdgpu_buffer_rsrc_t acc_t = tile_rsrc(P.buf[q ? 0 : 2] + (h << L), TBYTES);
+  const __amdgpu_buffer_rsrc_t acc_t = tile_rsrc(P.buf[q ? 0 : 2] + coff + (h << L), TBYTES);
   const uint32_t voff = (uint32_t)tid * 16u;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -666,17 +669,17 @@ hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu) {
 }
 
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items,
-                           int q, int set, int n_out, int* flags, int* err, hipStream_t st) {
+                           int q, int set, int n_out, int* flags, int* err, hipStream_t st, long colstride) {
   if (n_items <= 0) return hipSuccess;
   switch (L) {
 #define X(l)                                                                                     \
   case l:                                                                                        \
     if (imag)                                                                                    \
       hipLaunchKernelGGL((k_interval<l, true>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs,  \
-                         items, q, set, n_out, flags, err);                                             \
+                         items, q, set, n_out, flags, err, colstride);                                  \
     else                                                                                         \
       hipLaunchKernelGGL((k_interval<l, false>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs, \
-                         items, q, set, n_out, flags, err);                                             \
+                         items, q, set, n_out, flags, err, colstride);                                  \
     return hipGetLastError();
     X(10) X(11) X(12) X(13)
 #undef X

@@ -75,7 +75,10 @@ struct HostProblem {
   bool sm = false;           // this evolve runs the problem on that engine
   // dense eigen-propagator engine (dse_dense.hip): this evolve diagonalises the register instead
   bool dn = false;
-  bool side() const { return sm || dn; }  // not on the Chebyshev kernels in this evolve
+  // propagator-matrix mode (matrix_run): the context's single register, U = exp(-iH dt) built
+  // column by column, the outputs by repeated products
+  bool mx = false;
+  bool side() const { return sm || dn || mx; }  // not on the per-interval Chebyshev launches
   double2* sm_coef = nullptr;  // into dse_ctx::d_sm_coef
   int* sm_deg = nullptr;
   int final_bsel = 0;        // buffer holding the final state after dse_evolve
@@ -195,6 +198,9 @@ struct dse_ctx {
   // dense eigen-propagator engine (dse_dense.h): option "dense" 0 off, 1 when cheaper than the
   // Chebyshev propagator by the cost model of dense_cheaper (default), 2 for every eligible register
   int dense = 1;
+  // propagator-matrix mode for a context holding one register on a uniform grid: 0 off, 1 when
+  // the model of matrix_cheaper says so (default), 2 whenever eligible
+  int matrix = 1;
   hipStream_t dense_stream = nullptr;
   rocblas_handle blas = nullptr;
 };
@@ -1188,6 +1194,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     ctx->dbg = (int)value;
   } else if (k == "small") {  // registers of <= 9 qubits on the one-wave engine (dse_small.hip)
     ctx->small = value != 0.0;
+  } else if (k == "matrix") {  // propagator-matrix mode: 0 off, 1 auto, 2 always (when eligible)
+    if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "matrix must be 0, 1 or 2");
+    ctx->matrix = (int)value;
   } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
     if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "dense must be 0, 1 or 2");
     ctx->dense = (int)value;
@@ -1803,6 +1812,148 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
   return DSE_OK;
 }
 
+// ---- propagator-matrix mode ----------------------------------------------------------------
+// One evolution alone in a context runs its Chebyshev terms on one workgroup per tile: a chain of
+// ~alpha t_final + 30 (n_t - 1) terms at ~11 us each on one CU (config 2, N = 12: ~9e3 terms,
+// ~0.1 s) while the other 255 CUs idle.  On a uniform grid the whole evolution is psi_j =
+// U^j psi_0 with U = exp(-iH dt): U's 2^n columns are independent Chebyshev evolutions over one
+// interval (k_interval in column mode: 2^n workgroups, the whole chip), then the outputs are
+// n_t - 1 dependent products psi_{j+1} = U psi_j (rocBLAS zgemv, HBM-bound) and one observable
+// launch over all states.
+bool matrix_eligible(const HostProblem& P, const double* t, int n_t, double* dt_out) {
+  if (P.shard_bits != 0 || P.n_tiles != 1 || !interval_supported(P.L) || n_t < 17) return false;
+  if (P.n_local > 13) return false;
+  const double dt = (t[n_t - 1] - t[0]) / (n_t - 1);
+  for (int i = 1; i < n_t; ++i)
+    if (std::fabs((t[i] - t[i - 1]) - dt) > 1e-9 * dt) return false;
+  *dt_out = dt;
+  return true;
+}
+
+// seconds: the chain on one workgroup (~11.4 us per term at 2^12 amplitudes, linear in the tile)
+// against the column build spread over the chip (2 workgroups per CU below 2^13) plus n_t - 1
+// matrix-vector products at ~5 TB/s
+bool matrix_cheaper(const HostProblem& P, double dt, int n_t, int n_cu) {
+  const double dim = std::ldexp(1.0, P.n_local);
+  const double alpha = 0.5 * (P.e_max - P.e_min);
+  const double z = alpha * dt;
+  const double deg1 = z + 12.0 * std::cbrt(z + 1.0) + 20.0;
+  const double t_term = 11.4e-6 * std::max(dim / 4096.0, 0.25);
+  const double chain = (n_t - 1) * deg1 * t_term;
+  const double slots = (double)n_cu * (P.L < 13 ? 2.0 : 1.0);
+  const double build = std::ceil(dim / slots) * deg1 * t_term;
+  const double chain_u = (n_t - 1) * dim * dim * 16.0 / 5e12;
+  return build + chain_u < chain;
+}
+
+int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double tol, double* obs_out,
+               double* h_apps) {
+  HostProblem& P = ctx->probs[pi];
+  const int n = P.n_local;
+  const size_t dim = size_t(1) << n;
+  if (!ctx->blas && rocblas_create_handle(&ctx->blas) != rocblas_status_success)
+    return fail(ctx, DSE_ERR_HIP, "rocblas_create_handle failed");
+  hipStream_t st = ctx->lanes[0].stream;
+  if (rocblas_set_stream(ctx->blas, st) != rocblas_status_success)
+    return fail(ctx, DSE_ERR_HIP, "rocblas_set_stream failed");
+  // Chebyshev coefficients of one interval dt (one set, one output)
+  const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
+  const double beta = 0.5 * (P.e_max + P.e_min);
+  const double z = alpha * dt;
+  const int kmax = (int)std::ceil(z + 12.0 * std::cbrt(z + 1.0) + 60.0);
+  if (kmax > ctx->max_degree) return fail(ctx, DSE_ERR_CONVERGENCE, "Chebyshev degree exceeds max_degree");
+  std::vector<double> J(kmax + 1);
+  int deg = 1;
+  if (dse_bessel_j(z, kmax, J.data(), tol, &deg) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
+  std::vector<double2> row(deg + 2, make_double2(0.0, 0.0));
+  row[0] = make_double2((double)deg, 0.0);
+  {
+    const std::complex<double> e(std::cos(-beta * dt), std::sin(-beta * dt));
+    std::complex<double> mi(1.0, 0.0);
+    for (int k = 0; k <= deg; ++k) {
+      const std::complex<double> a = e * mi * ((k == 0 ? 1.0 : 2.0) * J[k]);
+      row[1 + k] = make_double2(a.real(), a.imag());
+      mi *= std::complex<double>(0.0, -1.0);
+    }
+  }
+  DevArena ar;
+  double2* B0 = ar.get<double2>(dim * dim);        // columns: e_c, then scratch
+  double2* U = ar.get<double2>(dim * dim);         // columns: U e_c
+  double2* S = ar.get<double2>(dim * (size_t)n_t);  // psi(t_j), consecutive
+  double2* d_row = ar.get<double2>(row.size());
+  DevProb* d_p = ar.get<DevProb>(1);
+  int2* d_items = ar.get<int2>(dim);
+  BasisInit* d_init = ar.get<BasisInit>(dim);
+  int* d_err = ar.get<int>(1);
+  double* d_obs = ar.get<double>((size_t)n_t * 8);
+  DenseProb* d_desc = ar.get<DenseProb>(1);
+  if (!B0 || !U || !S || !d_row || !d_p || !d_items || !d_init || !d_err || !d_obs || !d_desc)
+    return fail(ctx, DSE_ERR_OOM, "propagator-matrix mode: allocation failed");
+  DevProb d = ctx->h_desc[pi];
+  d.buf[0] = B0;
+  d.buf[1] = B0;
+  d.buf[2] = U;
+  d.coef = d_row;
+  d.kcap1 = deg + 1;
+  d.degree = deg;
+  d.beta = beta;
+  d.s1 = 1.0 / alpha;
+  d.n_acc = 1;
+  d.xacc_q = 0;
+  std::vector<int2> items(dim);
+  std::vector<BasisInit> init(dim);
+  for (size_t c = 0; c < dim; ++c) {
+    items[c] = make_int2(0, (int)c);
+    init[c].ptr = B0 + c * dim;
+    init[c].n = dim;
+    init[c].one_at = (int64_t)c;
+  }
+  HIPC(hipMemcpyAsync(d_row, row.data(), row.size() * sizeof(double2), hipMemcpyHostToDevice, st));
+  HIPC(hipMemcpyAsync(d_p, &d, sizeof(DevProb), hipMemcpyHostToDevice, st));
+  HIPC(hipMemcpyAsync(d_items, items.data(), dim * sizeof(int2), hipMemcpyHostToDevice, st));
+  HIPC(hipMemcpyAsync(d_init, init.data(), dim * sizeof(BasisInit), hipMemcpyHostToDevice, st));
+  HIPC(hipMemsetAsync(d_err, 0, sizeof(int), st));
+  HIPC(launch_basis_init(d_init, (int)dim, dim, st));
+  HIPC(launch_interval(P.L, P.imag, d_p, d_items, (int)dim, 0, 0, 1, d_err, d_err, st, (long)dim));
+  // psi_0 = e_x0, psi_1 = U e_x0 (column x0), psi_{j+1} = U psi_j
+  HIPC(hipMemsetAsync(S, 0, dim * sizeof(double2), st));
+  static const double2 one_c = {1.0, 0.0};
+  HIPC(hipMemcpyAsync(S + P.psi0, &one_c, sizeof(double2), hipMemcpyHostToDevice, st));
+  HIPC(hipMemcpyAsync(S + dim, U + P.psi0 * dim, dim * sizeof(double2), hipMemcpyDeviceToDevice, st));
+  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
+  for (int j = 1; j + 1 < n_t; ++j) {
+    const rocblas_status rs = rocblas_zgemv(ctx->blas, rocblas_operation_none, (rocblas_int)dim, (rocblas_int)dim,
+                                            &one, reinterpret_cast<const rocblas_double_complex*>(U),
+                                            (rocblas_int)dim,
+                                            reinterpret_cast<const rocblas_double_complex*>(S + dim * j), 1,
+                                            &zero, reinterpret_cast<rocblas_double_complex*>(S + dim * (j + 1)), 1);
+    if (rs != rocblas_status_success)
+      return fail(ctx, DSE_ERR_HIP, "rocblas zgemv failed (status " + std::to_string((int)rs) + ")");
+  }
+  DenseProb D = {};
+  D.n = n;
+  D.rot = 0;
+  D.sea_mask = P.sea_mask;
+  D.rare_bit = P.rare_bit;
+  D.n_sea = __builtin_popcountll(P.sea_mask);
+  D.x0 = P.psi0;
+  D.obs = d_obs;
+  HIPC(hipMemcpyAsync(d_desc, &D, sizeof(DenseProb), hipMemcpyHostToDevice, st));
+  HIPC(launch_state_obs(d_desc, (int)dim, S, n_t, 0, st));
+  HIPC(hipMemcpyAsync(P.buf[0], S + dim * (size_t)(n_t - 1), dim * sizeof(double2), hipMemcpyDeviceToDevice, st));
+  std::vector<double> h((size_t)n_t * 8);
+  int herr = 0;
+  HIPC(hipMemcpyAsync(h.data(), d_obs, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  if (herr) return fail(ctx, DSE_ERR_HIP, "propagator-matrix mode: column build failed");
+  for (int ti = 0; ti < n_t; ++ti)
+    finish_obs(P, h.data() + (size_t)ti * 8, obs_out + (size_t)pi * DSE_N_OBS * n_t + ti, (size_t)n_t);
+  P.degree = deg;
+  *h_apps = (double)deg * (double)dim;
+  return DSE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1910,10 +2061,28 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     any_dense = any_dense || P.dn;
   }
   for (auto& P : ctx->probs) {
+    P.mx = false;
     P.sm = !P.dn && ctx->small && P.shard_bits == 0 && P.n_local <= kSmallMaxQubits;
     any_small = any_small || P.sm;
-    any_big = any_big || !P.side();
   }
+  // a context whose Chebyshev work is one register: propagator-matrix mode (matrix_run) when the
+  // persistent kernel is allowed and the model prefers it
+  int matrix_pi = -1;
+  double matrix_dt = 0.0;
+  {
+    int n_cheb = 0, last = -1;
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+      if (!ctx->probs[pi].side()) ++n_cheb, last = (int)pi;
+    if (n_cheb == 1 && ctx->matrix && ctx->persistent) {
+      HostProblem& P = ctx->probs[last];
+      if (matrix_eligible(P, t, n_t, &matrix_dt) &&
+          (ctx->matrix == 2 || matrix_cheaper(P, matrix_dt, n_t, ctx->n_cu))) {
+        P.mx = true;
+        matrix_pi = last;
+      }
+    }
+  }
+  for (auto& P : ctx->probs) any_big = any_big || !P.side();
   bool persistent = ctx->persistent != 0;
   bool any_dist = false;
   for (auto& P : ctx->probs) {
@@ -2334,6 +2503,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
 
   double dense_ms = 0.0, dense_eig_ms = 0.0;
   if (any_dense && (rc = dense_run(ctx, t, n_t, obs_out, &dense_ms, &dense_eig_ms))) return rc;
+  double matrix_happl = 0.0;
+  if (matrix_pi >= 0 && (rc = matrix_run(ctx, matrix_pi, t, n_t, matrix_dt, tol, obs_out, &matrix_happl))) return rc;
   phase("psi0/small");
   const size_t chunk = (size_t)std::max<int64_t>(M, std::min<int64_t>(
       n_t, std::max<int64_t>(1, (int64_t)(256ll << 20) / (ctx->total_items * 64))));
@@ -2538,7 +2709,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   ctx->evolved = true;
 
   if (stats) {
-    double happl = small_happl;
+    double happl = small_happl + matrix_happl;
     for (auto& P : ctx->probs)
       if (!P.side()) happl += (double)P.degree * n_groups;
     std::memset(stats, 0, sizeof(*stats));
@@ -2548,7 +2719,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->h_flops = all_flops;
     stats->timed_flops = flops_timed;
     stats->timed_amp_terms = amps_timed;
-    stats->mode = !any_big ? (any_dense ? 4 : 3) : (persistent ? 1 : (used_wht ? 2 : 0));
+    stats->mode = matrix_pi >= 0 ? 5 : (!any_big ? (any_dense ? 4 : 3) : (persistent ? 1 : (used_wht ? 2 : 0)));
     int n_dense = 0;
     for (auto& P : ctx->probs) n_dense += P.dn ? 1 : 0;
     stats->dense_problems = n_dense;
@@ -2560,7 +2731,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->timed_bytes = bytes_timed;
     stats->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
     for (auto& P : ctx->probs)
-      if (P.sm) max_deg = std::max(max_deg, P.degree);
+      if (P.sm || P.mx) max_deg = std::max(max_deg, P.degree);
     stats->max_degree = max_deg;
     stats->n_intervals = n_t - 1;
     stats->tile_bits = ctx->probs.empty() ? 0 : ctx->probs.front().L;
