@@ -2042,6 +2042,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   for (int i = 1; i < n_t; ++i)
     if (!(t[i] > t[i - 1])) return fail(ctx, DSE_ERR_ARG, "times must be strictly increasing");
   HIPC(hipSetDevice(ctx->device));
+  // timing-event records of an earlier call that ended early (an error, or the hand-off timeout
+  // dse_evolve re-runs) are dropped: their per-launch counters lived in that call
+  for (auto& ln : ctx->lanes) ln.ev_used[0] = ln.ev_used[1] = 0;
   int rc = prepare(ctx);
   if (rc) return rc;
   ctx->xbytes = 0.0;
