@@ -58,3 +58,19 @@ hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const doub
                               int tb, double tau_last, hipStream_t st);
 
 }  // namespace dse
+
+namespace dse {
+
+// ---- propagator-matrix mode (dse_runtime.hip matrix_run): y = U x for the column-built
+// U = exp(-iH dt) of a register whose rotated form is symmetric, U_cr = s_r s_c U_rc with
+// s_x = (-1)^popcount(x) (imaginary drives; s = 1 for real ones).  Only the 128 x 128 tiles on or
+// above the diagonal are read (half the matrix): tile (I, J) adds U_IJ x_J to row block I and,
+// below the diagonal by symmetry, s (U_IJ^T (s x_I)) to row block J.  Per-tile partial sums
+// partial[B][k][128] (k = the other block index) are summed in fixed order by the reduce kernel:
+// deterministic, no atomics.
+constexpr int kSymvBlock = 128;
+hipError_t launch_symv(const double2* U, int dim, const double2* x, double2* partial, int parity,
+                       hipStream_t st);
+hipError_t launch_symv_reduce(const double2* partial, int dim, double2* y, hipStream_t st);
+
+}  // namespace dse

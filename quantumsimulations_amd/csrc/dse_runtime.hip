@@ -1920,8 +1920,17 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
   static const double2 one_c = {1.0, 0.0};
   HIPC(hipMemcpyAsync(S + P.psi0, &one_c, sizeof(double2), hipMemcpyHostToDevice, st));
   HIPC(hipMemcpyAsync(S + dim, U + P.psi0 * dim, dim * sizeof(double2), hipMemcpyDeviceToDevice, st));
+  // U's rotated form is symmetric when the drives are all imaginary (parity twist s_r s_c) or all
+  // real: half-matrix products (k_symv); otherwise rocBLAS zgemv on the whole matrix
+  const bool sym = dense_eligible(P);
+  double2* part = sym ? ar.get<double2>((dim / kSymvBlock) * dim) : nullptr;
+  if (sym && !part) return fail(ctx, DSE_ERR_OOM, "propagator-matrix mode: allocation failed");
   const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
-  for (int j = 1; j + 1 < n_t; ++j) {
+  for (int j = 1; j + 1 < n_t && sym; ++j) {
+    HIPC(launch_symv(U, (int)dim, S + dim * j, part, P.imag ? 1 : 0, st));
+    HIPC(launch_symv_reduce(part, (int)dim, S + dim * (j + 1), st));
+  }
+  for (int j = 1; j + 1 < n_t && !sym; ++j) {
     const rocblas_status rs = rocblas_zgemv(ctx->blas, rocblas_operation_none, (rocblas_int)dim, (rocblas_int)dim,
                                             &one, reinterpret_cast<const rocblas_double_complex*>(U),
                                             (rocblas_int)dim,

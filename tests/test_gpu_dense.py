@@ -107,3 +107,25 @@ def test_cost_model_keeps_short_n14_grid_on_chebyshev(engine):
     _, st = engine.evolve(t)
     engine.clear()
     assert st["dense_problems"] == 0 and st["mode"] == 1
+
+
+def test_dense_full_grid_n14_matches_chebyshev_prefix(engine):
+    """BASELINE's "(full sweep)" engine at config 3's size: the dense engine on the WHOLE reference
+    grid (30 s, 20 000 outputs; dim 16384 / 8192 eigendecompositions) for the 3 variants at 150 kHz
+    agrees with the persistent Chebyshev kernel on the grid's first intervals."""
+    t_ref = np.linspace(0.0, 30.0, 20000)
+    params = [sweep_point_params(13, 150e3, v, 30.0, 20000) for v in VARIANTS]
+    engine.clear()
+    for p in params:
+        engine.add(pb.build_problem(p))
+    obs, st = engine.evolve(t_ref)
+    engine.clear()
+    assert st["dense_problems"] == 3
+    np.testing.assert_allclose(obs[:, 6], 1.0, atol=1e-10)
+    K = 3
+    for p in params:
+        engine.add(pb.build_problem(p))
+    ch, st2 = engine.evolve(t_ref[:K + 1])
+    engine.clear()
+    assert st2["dense_problems"] == 0 and st2["mode"] == 1
+    assert np.max(np.abs(obs[:, :, :K + 1] - ch)) < 1e-9
