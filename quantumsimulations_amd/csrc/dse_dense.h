@@ -63,14 +63,29 @@ namespace dse {
 
 // ---- propagator-matrix mode (dse_runtime.hip matrix_run): y = U x for the column-built
 // U = exp(-iH dt) of a register whose rotated form is symmetric, U_cr = s_r s_c U_rc with
-// s_x = (-1)^popcount(x) (imaginary drives; s = 1 for real ones).  Only the 128 x 128 tiles on or
-// above the diagonal are read (half the matrix): tile (I, J) adds U_IJ x_J to row block I and,
+// s_x = (-1)^popcount(x) (imaginary drives; s = 1 for real ones).  Only the kSymvBlock^2 tiles on
+// or above the diagonal are read (half the matrix): tile (I, J) adds U_IJ x_J to row block I and,
 // below the diagonal by symmetry, s (U_IJ^T (s x_I)) to row block J.  Per-tile partial sums
-// partial[B][k][128] (k = the other block index) are summed in fixed order by the reduce kernel:
+// partial[B][k][kSymvBlock] (k = the other block index) are summed in fixed order by the reduce kernel:
 // deterministic, no atomics.
-constexpr int kSymvBlock = 128;
+constexpr int kSymvBlock = 64;
+// tile storage of U for k_symv: the kSymvBlock^2 tiles (I, J), I <= J, in the row-major order of the
+// upper triangle of nb x nb blocks, each column-major (64 KiB contiguous)
+__host__ __device__ inline size_t symv_tile_index(int I, int J, int nb) {
+  return (size_t)I * nb - (size_t)I * (I - 1) / 2 + (size_t)(J - I);
+}
 hipError_t launch_symv(const double2* U, int dim, const double2* x, double2* partial, int parity,
                        hipStream_t st);
 hipError_t launch_symv_reduce(const double2* partial, int dim, double2* y, hipStream_t st);
+
+// Column build in real arithmetic (dse_matrix.hip, k_ucols): U e_c for columns col0 .. col0 +
+// n_cols - 1 of a one-tile register (n == L, drives all imaginary (rot = 1) or all real (rot = 0)),
+// one workgroup per column.  probs: one DevProb with beta and s1 = 1 / alpha of the interval;
+// cf[k] = (-1)^{floor(k/2)} (2 - delta_k0) J_k(alpha dt), k = 0..deg; (phr, phi) = e^{-i beta dt}.
+// U in the computational frame, in k_symv's tile storage (the tiles on and above the diagonal);
+// column c1 also whole (2^L amplitudes) into psi1.
+bool ucols_supported(int L);
+hipError_t launch_ucols(int L, const struct DevProb* probs, const double* cf, int deg, int rot, double phr,
+                        double phi, double2* U, int n_cols, int col0, int c1, double2* psi1, hipStream_t st);
 
 }  // namespace dse

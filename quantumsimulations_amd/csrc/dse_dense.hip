@@ -188,112 +188,3 @@ hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const doub
 }
 
 }  // namespace dse
-
-namespace dse {
-namespace {
-
-// One 128 x 128 tile (I, J), I <= J, of the column-major complex matrix U (ld = dim); 256 threads:
-// wave w takes columns w * 32 .. w * 32 + 31 of the tile, lane l rows l and l + 64.  The two
-// row-halves' loads of 8 columns are issued together (16 x 16-B loads in flight per lane).
-__global__ void __launch_bounds__(256)
-k_symv(const double2* __restrict__ U, int dim, const double2* __restrict__ x, double2* __restrict__ partial,
-       int parity) {
-  constexpr int BS = kSymvBlock;
-  const int nb = dim / BS;
-  // blockIdx.x -> (I, J) with I <= J, row-major over the upper triangle
-  int I = 0, rem = (int)blockIdx.x;
-  while (rem >= nb - I) rem -= nb - I, ++I;
-  const int J = I + rem;
-  __shared__ double2 xs[2][BS];   // x_J, s * x_I
-  __shared__ double2 red[4][BS];  // per-wave direct partials
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid < BS) {
-    xs[0][tid] = x[J * BS + tid];
-    const int r = I * BS + tid;
-    const double2 v = x[r];
-    const double s = (parity && (__popc(r) & 1)) ? -1.0 : 1.0;
-    xs[1][tid] = make_double2(s * v.x, s * v.y);
-  }
-  __syncthreads();
-  const bool off = I < J;
-  const double2* col0 = U + (size_t)(J * BS + w * 32) * dim + (size_t)I * BS;
-  double2 a0 = make_double2(0.0, 0.0), a1 = make_double2(0.0, 0.0);  // direct: rows lane, lane + 64
-  const double2 sx0 = xs[1][lane], sx1 = xs[1][lane + 64];
-  double2 tsum = make_double2(0.0, 0.0);  // transposed sum of this lane's column (lane < 32)
-#pragma unroll 1
-  for (int c0 = 0; c0 < 32; c0 += 8) {
-    double2 u0[8], u1[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const double2* col = col0 + (size_t)(c0 + c) * dim;
-      u0[c] = col[lane];
-      u1[c] = col[lane + 64];
-    }
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const double2 xj = xs[0][w * 32 + c0 + c];
-      a0.x = fma(u0[c].x, xj.x, fma(-u0[c].y, xj.y, a0.x));
-      a0.y = fma(u0[c].x, xj.y, fma(u0[c].y, xj.x, a0.y));
-      a1.x = fma(u1[c].x, xj.x, fma(-u1[c].y, xj.y, a1.x));
-      a1.y = fma(u1[c].x, xj.y, fma(u1[c].y, xj.x, a1.y));
-      if (off) {  // sum_r U_rc (s x_I)_r over the tile's 128 rows: lane partial, then the wave's
-        double px = u0[c].x * sx0.x - u0[c].y * sx0.y + u1[c].x * sx1.x - u1[c].y * sx1.y;
-        double py = u0[c].x * sx0.y + u0[c].y * sx0.x + u1[c].x * sx1.y + u1[c].y * sx1.x;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          px += __shfl_xor(px, o, 64);
-          py += __shfl_xor(py, o, 64);
-        }
-        if (lane == c0 + c) tsum = make_double2(px, py);
-      }
-    }
-  }
-  red[w][lane] = a0;
-  red[w][lane + 64] = a1;
-  __syncthreads();
-  // direct partial of row block I from this tile (contributor k = J), fixed wave order
-  if (tid < BS) {
-    double2 s = red[0][tid];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) s.x += red[q][tid].x, s.y += red[q][tid].y;
-    partial[((size_t)I * nb + J) * BS + tid] = s;
-  }
-  // transposed partial of row block J (contributor k = I): s_c * sum, column c = w * 32 + lane
-  if (off && lane < 32) {
-    const int c = w * 32 + lane;
-    const double sc = (parity && (__popc(J * BS + c) & 1)) ? -1.0 : 1.0;
-    partial[((size_t)J * nb + I) * BS + c] = make_double2(sc * tsum.x, sc * tsum.y);
-  }
-}
-
-__global__ void __launch_bounds__(256)
-k_symv_reduce(const double2* __restrict__ partial, int dim, double2* __restrict__ y) {
-  constexpr int BS = kSymvBlock;
-  const int nb = dim / BS;
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= dim) return;
-  const int B = r / BS, rr = r % BS;
-  double2 s = make_double2(0.0, 0.0);
-  for (int k = 0; k < nb; ++k) {
-    const double2 v = partial[((size_t)B * nb + k) * BS + rr];
-    s.x += v.x;
-    s.y += v.y;
-  }
-  y[r] = s;
-}
-
-}  // namespace
-
-hipError_t launch_symv(const double2* U, int dim, const double2* x, double2* partial, int parity,
-                       hipStream_t st) {
-  const int nb = dim / kSymvBlock;
-  hipLaunchKernelGGL(k_symv, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, U, dim, x, partial, parity);
-  return hipGetLastError();
-}
-
-hipError_t launch_symv_reduce(const double2* partial, int dim, double2* y, hipStream_t st) {
-  hipLaunchKernelGGL(k_symv_reduce, dim3((dim + 255) / 256), dim3(256), 0, st, partial, dim, y);
-  return hipGetLastError();
-}
-
-}  // namespace dse

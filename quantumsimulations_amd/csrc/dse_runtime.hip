@@ -201,6 +201,11 @@ struct dse_ctx {
   // propagator-matrix mode for a context holding one register on a uniform grid: 0 off, 1 when
   // the model of matrix_cheaper says so (default), 2 whenever eligible
   int matrix = 1;
+  // matrix mode's device buffers (U, the states, the products' partial sums, tables), kept across
+  // evolves of the same register size (simulate_rare calls one register at a time; a 2^12 register
+  // holds 256 MiB of U) and released by dse_destroy or when a larger register needs more
+  unsigned char* d_mx = nullptr;
+  size_t mx_cap = 0;
   hipStream_t dense_stream = nullptr;
   rocblas_handle blas = nullptr;
 };
@@ -1132,6 +1137,7 @@ void dse_destroy(dse_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)sync_all(ctx);
   free_device(ctx);
+  if (ctx->d_mx) (void)hipFree(ctx->d_mx), ctx->d_mx = nullptr;
   destroy_lanes(ctx);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   delete ctx;
@@ -1851,11 +1857,7 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
   HostProblem& P = ctx->probs[pi];
   const int n = P.n_local;
   const size_t dim = size_t(1) << n;
-  if (!ctx->blas && rocblas_create_handle(&ctx->blas) != rocblas_status_success)
-    return fail(ctx, DSE_ERR_HIP, "rocblas_create_handle failed");
   hipStream_t st = ctx->lanes[0].stream;
-  if (rocblas_set_stream(ctx->blas, st) != rocblas_status_success)
-    return fail(ctx, DSE_ERR_HIP, "rocblas_set_stream failed");
   // Chebyshev coefficients of one interval dt (one set, one output)
   const double alpha = std::max(0.5 * (P.e_max - P.e_min), 1e-300);
   const double beta = 0.5 * (P.e_max + P.e_min);
@@ -1865,72 +1867,108 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
   std::vector<double> J(kmax + 1);
   int deg = 1;
   if (dse_bessel_j(z, kmax, J.data(), tol, &deg) != DSE_OK) return fail(ctx, DSE_ERR_ARG, "bessel failed");
-  std::vector<double2> row(deg + 2, make_double2(0.0, 0.0));
+  // U's rotated form is symmetric when the drives are all imaginary (parity twist s_r s_c) or all
+  // real: the column build runs in real arithmetic (k_ucols) and the products read the tiles on and
+  // above the diagonal (k_symv); otherwise the complex column build and rocBLAS zgemv on the whole
+  // column-major matrix
+  const bool real_build = dense_eligible(P) && ucols_supported(P.L) && P.n_local == P.L;
+  std::vector<double2> row(deg + 2, make_double2(0.0, 0.0));  // complex build: a_k
+  std::vector<double> cf(deg + 1);                               // real build: (-1)^{k/2} c_k
   row[0] = make_double2((double)deg, 0.0);
   {
     const std::complex<double> e(std::cos(-beta * dt), std::sin(-beta * dt));
     std::complex<double> mi(1.0, 0.0);
     for (int k = 0; k <= deg; ++k) {
-      const std::complex<double> a = e * mi * ((k == 0 ? 1.0 : 2.0) * J[k]);
+      const double ck = (k == 0 ? 1.0 : 2.0) * J[k];
+      const std::complex<double> a = e * mi * ck;
       row[1 + k] = make_double2(a.real(), a.imag());
+      cf[k] = ((k >> 1) & 1) ? -ck : ck;
       mi *= std::complex<double>(0.0, -1.0);
     }
   }
-  DevArena ar;
-  double2* B0 = ar.get<double2>(dim * dim);        // columns: e_c, then scratch
-  double2* U = ar.get<double2>(dim * dim);         // columns: U e_c
-  double2* S = ar.get<double2>(dim * (size_t)n_t);  // psi(t_j), consecutive
-  double2* d_row = ar.get<double2>(row.size());
-  DevProb* d_p = ar.get<DevProb>(1);
-  int2* d_items = ar.get<int2>(dim);
-  BasisInit* d_init = ar.get<BasisInit>(dim);
-  int* d_err = ar.get<int>(1);
-  double* d_obs = ar.get<double>((size_t)n_t * 8);
-  DenseProb* d_desc = ar.get<DenseProb>(1);
-  if (!B0 || !U || !S || !d_row || !d_p || !d_items || !d_init || !d_err || !d_obs || !d_desc)
-    return fail(ctx, DSE_ERR_OOM, "propagator-matrix mode: allocation failed");
+  // device buffers: kept in the context between calls (ctx->d_mx)
+  const size_t nb = dim / kSymvBlock;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + std::max<size_t>(bytes, 1), 256);
+    return o;
+  };
+  const size_t u_elems = real_build ? nb * (nb + 1) / 2 * kSymvBlock * kSymvBlock : dim * dim;
+  const size_t oU = take(u_elems * sizeof(double2)), oS = take(dim * (size_t)n_t * sizeof(double2)),
+               oPart = take(real_build ? nb * dim * sizeof(double2) : 0), oObs = take((size_t)n_t * 8 * sizeof(double)),
+               oDesc = take(sizeof(DenseProb)), oProb = take(sizeof(DevProb)),
+               oCoef = take(std::max(row.size() * sizeof(double2), cf.size() * sizeof(double))), oErr = take(sizeof(int));
+  if (off > ctx->mx_cap) {
+    if (ctx->d_mx) (void)hipFree(ctx->d_mx), ctx->d_mx = nullptr;
+    ctx->mx_cap = 0;
+    if (hipMalloc(&ctx->d_mx, off) != hipSuccess) return fail(ctx, DSE_ERR_OOM, "propagator-matrix mode: allocation failed");
+    ctx->mx_cap = off;
+  }
+  unsigned char* base = ctx->d_mx;
+  double2* U = reinterpret_cast<double2*>(base + oU);     // tiles (real build) or columns: U e_c
+  double2* S = reinterpret_cast<double2*>(base + oS);     // psi(t_j), consecutive
+  double2* part = real_build ? reinterpret_cast<double2*>(base + oPart) : nullptr;
+  double* d_obs = reinterpret_cast<double*>(base + oObs);
+  DenseProb* d_desc = reinterpret_cast<DenseProb*>(base + oDesc);
+  DevProb* d_p = reinterpret_cast<DevProb*>(base + oProb);
+  int* d_err = reinterpret_cast<int*>(base + oErr);
   DevProb d = ctx->h_desc[pi];
-  d.buf[0] = B0;
-  d.buf[1] = B0;
-  d.buf[2] = U;
-  d.coef = d_row;
-  d.kcap1 = deg + 1;
-  d.degree = deg;
   d.beta = beta;
   d.s1 = 1.0 / alpha;
-  d.n_acc = 1;
-  d.xacc_q = 0;
-  std::vector<int2> items(dim);
-  std::vector<BasisInit> init(dim);
-  for (size_t c = 0; c < dim; ++c) {
-    items[c] = make_int2(0, (int)c);
-    init[c].ptr = B0 + c * dim;
-    init[c].n = dim;
-    init[c].one_at = (int64_t)c;
-  }
-  HIPC(hipMemcpyAsync(d_row, row.data(), row.size() * sizeof(double2), hipMemcpyHostToDevice, st));
-  HIPC(hipMemcpyAsync(d_p, &d, sizeof(DevProb), hipMemcpyHostToDevice, st));
-  HIPC(hipMemcpyAsync(d_items, items.data(), dim * sizeof(int2), hipMemcpyHostToDevice, st));
-  HIPC(hipMemcpyAsync(d_init, init.data(), dim * sizeof(BasisInit), hipMemcpyHostToDevice, st));
+  d.degree = deg;
   HIPC(hipMemsetAsync(d_err, 0, sizeof(int), st));
-  HIPC(launch_basis_init(d_init, (int)dim, dim, st));
-  HIPC(launch_interval(P.L, P.imag, d_p, d_items, (int)dim, 0, 0, 1, d_err, d_err, st, (long)dim));
+  DevArena ar;  // complex build only: the basis columns
+  if (real_build) {
+    double* d_cf = reinterpret_cast<double*>(base + oCoef);
+    HIPC(hipMemcpyAsync(d_cf, cf.data(), cf.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_p, &d, sizeof(DevProb), hipMemcpyHostToDevice, st));
+    HIPC(launch_ucols(P.L, d_p, d_cf, deg, P.imag ? 1 : 0, std::cos(-beta * dt), std::sin(-beta * dt), U, (int)dim,
+                      0, (int)P.psi0, S + dim, st));
+  } else {
+    if (!ctx->blas && rocblas_create_handle(&ctx->blas) != rocblas_status_success)
+      return fail(ctx, DSE_ERR_HIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(ctx->blas, st) != rocblas_status_success)
+      return fail(ctx, DSE_ERR_HIP, "rocblas_set_stream failed");
+    double2* B0 = ar.get<double2>(dim * dim);  // columns: e_c, then scratch
+    int2* d_items = ar.get<int2>(dim);
+    BasisInit* d_init = ar.get<BasisInit>(dim);
+    if (!B0 || !d_items || !d_init) return fail(ctx, DSE_ERR_OOM, "propagator-matrix mode: allocation failed");
+    double2* d_row = reinterpret_cast<double2*>(base + oCoef);
+    d.buf[0] = B0;
+    d.buf[1] = B0;
+    d.buf[2] = U;
+    d.coef = d_row;
+    d.kcap1 = deg + 1;
+    d.n_acc = 1;
+    d.xacc_q = 0;
+    std::vector<int2> items(dim);
+    std::vector<BasisInit> init(dim);
+    for (size_t c = 0; c < dim; ++c) {
+      items[c] = make_int2(0, (int)c);
+      init[c].ptr = B0 + c * dim;
+      init[c].n = dim;
+      init[c].one_at = (int64_t)c;
+    }
+    HIPC(hipMemcpyAsync(d_row, row.data(), row.size() * sizeof(double2), hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_p, &d, sizeof(DevProb), hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_items, items.data(), dim * sizeof(int2), hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_init, init.data(), dim * sizeof(BasisInit), hipMemcpyHostToDevice, st));
+    HIPC(launch_basis_init(d_init, (int)dim, dim, st));
+    HIPC(launch_interval(P.L, P.imag, d_p, d_items, (int)dim, 0, 0, 1, d_err, d_err, st, (long)dim));
+  }
   // psi_0 = e_x0, psi_1 = U e_x0 (column x0), psi_{j+1} = U psi_j
   HIPC(hipMemsetAsync(S, 0, dim * sizeof(double2), st));
   static const double2 one_c = {1.0, 0.0};
   HIPC(hipMemcpyAsync(S + P.psi0, &one_c, sizeof(double2), hipMemcpyHostToDevice, st));
-  HIPC(hipMemcpyAsync(S + dim, U + P.psi0 * dim, dim * sizeof(double2), hipMemcpyDeviceToDevice, st));
-  // U's rotated form is symmetric when the drives are all imaginary (parity twist s_r s_c) or all
-  // real: half-matrix products (k_symv); otherwise rocBLAS zgemv on the whole matrix
-  const bool sym = dense_eligible(P);
-  double2* part = sym ? ar.get<double2>((dim / kSymvBlock) * dim) : nullptr;
-  if (sym && !part) return fail(ctx, DSE_ERR_OOM, "propagator-matrix mode: allocation failed");
+  if (!real_build)  // (the real build wrote column x0 itself)
+    HIPC(hipMemcpyAsync(S + dim, U + P.psi0 * dim, dim * sizeof(double2), hipMemcpyDeviceToDevice, st));
   const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
-  for (int j = 1; j + 1 < n_t && sym; ++j) {
+  for (int j = 1; j + 1 < n_t && real_build; ++j) {
     HIPC(launch_symv(U, (int)dim, S + dim * j, part, P.imag ? 1 : 0, st));
     HIPC(launch_symv_reduce(part, (int)dim, S + dim * (j + 1), st));
   }
-  for (int j = 1; j + 1 < n_t && !sym; ++j) {
+  for (int j = 1; j + 1 < n_t && !real_build; ++j) {
     const rocblas_status rs = rocblas_zgemv(ctx->blas, rocblas_operation_none, (rocblas_int)dim, (rocblas_int)dim,
                                             &one, reinterpret_cast<const rocblas_double_complex*>(U),
                                             (rocblas_int)dim,

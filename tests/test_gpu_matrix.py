@@ -1,12 +1,16 @@
 """Propagator-matrix mode (dse_runtime.hip matrix_run): a context whose Chebyshev work is ONE
 register on a uniform grid -- BASELINE config 2, one simulate_rare call of the unmodified caller
-(sweep_sea_detuning.py:671-673) -- builds U = exp(-iH dt) column by column with the interval
-kernel in column mode (2^n workgroups over the chip instead of one), then psi_{j+1} = U psi_j.
+(sweep_sea_detuning.py:671-673) -- builds U = exp(-iH dt) column by column (2^n workgroups over the
+chip instead of one), then psi_{j+1} = U psi_j.  Imaginary (or real) drives: real-arithmetic column
+build k_ucols into tile storage + half-matrix products k_symv; mixed drives: the interval kernel in
+column mode + rocBLAS zgemv.
 
 * config 2 (N = 12 center_on, 2 ms / 201 outputs): mode 5, against the exact-eigh fixture of the
   reference-built H (1e-10) and the per-interval engine (option matrix = 0, 1e-11), same final state
 * N = 10 (center_on, n_sea = 9) and a shell_off register, forced: same traces as the per-interval
   engine
+* drive phases off pi/2 (complex drive coefficients): the complex build + zgemv, same traces as the
+  per-interval engine
 * a non-uniform grid or a second register keeps the per-interval kernels
 """
 import numpy as np
@@ -59,6 +63,16 @@ def test_matrix_mode_forced_matches_per_interval(engine, n_sea, variant):
     assert np.max(np.abs(mx - ch)) < 1e-11
     assert np.max(np.abs(s_mx[0] - s_ch[0])) < 1e-11
     np.testing.assert_allclose(mx[0, 6], 1.0, atol=1e-12)
+
+
+def test_matrix_mode_complex_drives_match_per_interval(engine):
+    t = np.linspace(0.0, 4e-4, 41)
+    p = sweep_point_params(9, 80e3, "center_on", float(t[-1]), len(t), phi_sea=0.3, phi_rare=1.1)
+    mx, st, s_mx = _run(engine, [p], t, 2)
+    assert st["mode"] == 5
+    ch, _, s_ch = _run(engine, [p], t, 0)
+    assert np.max(np.abs(mx - ch)) < 1e-11
+    assert np.max(np.abs(s_mx[0] - s_ch[0])) < 1e-11
 
 
 def test_matrix_mode_only_for_one_register_on_a_uniform_grid(engine):
