@@ -74,8 +74,10 @@ constexpr int kSymvBlock = 64;
 __host__ __device__ inline size_t symv_tile_index(int I, int J, int nb) {
   return (size_t)I * nb - (size_t)I * (I - 1) / 2 + (size_t)(J - I);
 }
+// cnt (nb zeroed ints) non-null: the reduction into y in the same launch (k_symv<FUSED>), counters
+// left zeroed; null: partials only, then launch_symv_reduce
 hipError_t launch_symv(const double2* U, int dim, const double2* x, double2* partial, int parity,
-                       hipStream_t st);
+                       hipStream_t st, int* cnt = nullptr, double2* y = nullptr);
 hipError_t launch_symv_reduce(const double2* partial, int dim, double2* y, hipStream_t st);
 
 // Column build in real arithmetic (dse_matrix.hip, k_ucols): U e_c for columns col0 .. col0 +

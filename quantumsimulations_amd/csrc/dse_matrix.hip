@@ -339,9 +339,16 @@ k_ucols(const DevProb* __restrict__ probs, const double* __restrict__ cf, int de
 // 8 halve the set, xor 4, 2, 1 finish it: 10 complex exchanges per chunk instead of 48).  Small
 // tiles (BS = 64: 2080 of 64 KiB at N = 12) spread the matrix evenly over the CUs (with 128 x 128
 // tiles 528 of 256 KiB left 16 CUs three tiles: the product took as long as those).
+//
+// FUSED: the reduction as well -- every workgroup counts itself in the agent-scope counters of its
+// two row blocks after an agent release (MI355X_MICROARCH.md, valid forms: plain stores, vmcnt(0)
+// per wave, barrier, lane-0 release, counter), and the workgroup whose add completes a block's count
+// (nb contributions) acquires and sums that block's partials in the fixed k order of k_symv_reduce,
+// then resets the counter for the next product: one launch per product instead of two.
+template <bool FUSED>
 __global__ void __launch_bounds__(256)
 k_symv(const double2* __restrict__ U, int dim, const double2* __restrict__ x, double2* __restrict__ partial,
-       int parity) {
+       int parity, int* __restrict__ cnt, double2* __restrict__ y) {
   constexpr int BS = kSymvBlock, RL = BS / 64, CW = BS / 4;
   const int nb = dim / BS;
   // blockIdx.x -> (I, J) with I <= J, row-major over the upper triangle
@@ -437,6 +444,49 @@ k_symv(const double2* __restrict__ U, int dim, const double2* __restrict__ x, do
     const double2 t = tr[w][lane];
     partial[((size_t)J * nb + I) * BS + c] = make_double2(sc * t.x, sc * t.y);
   }
+  if constexpr (FUSED) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int last = 0;
+      if (__hip_atomic_fetch_add(cnt + I, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) last |= 1;
+      if (off && __hip_atomic_fetch_add(cnt + J, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) last |= 2;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    const int last = s_last;
+    for (int which = 0; which < 2; ++which) {
+      if (!((last >> which) & 1)) continue;
+      const int B = which ? J : I;
+      // 256 threads: row tid % 64 of block B, quarter tid / 64 of the k range, then the quarters
+      const int rr = tid & 63, part = tid >> 6;
+      double2 a = make_double2(0.0, 0.0);
+      if (rr < BS) {
+        const int k0 = part * nb / 4, k1 = (part + 1) * nb / 4;
+        for (int k = k0; k < k1; ++k) {
+          const double2 v = partial[((size_t)B * nb + k) * BS + rr];
+          a.x += v.x;
+          a.y += v.y;
+        }
+      }
+      red[part][rr] = a;
+      __syncthreads();
+      if (part == 0 && rr < BS) {
+#pragma unroll
+        for (int q = 1; q < 4; ++q) a.x += red[q][rr].x, a.y += red[q][rr].y;
+        y[B * BS + rr] = a;
+      }
+      if (tid == 0) cnt[B] = 0;  // the next product is the next launch (stream order)
+      __syncthreads();
+    }
+  }
 }
 
 // y[r] = sum_k partial[r / BS][k][r % BS] in fixed k order: a workgroup of 256 threads takes 16
@@ -489,9 +539,13 @@ hipError_t launch_ucols(int L, const DevProb* probs, const double* cf, int deg, 
 }
 
 hipError_t launch_symv(const double2* U, int dim, const double2* x, double2* partial, int parity,
-                       hipStream_t st) {
+                       hipStream_t st, int* cnt, double2* y) {
   const int nb = dim / kSymvBlock;
-  hipLaunchKernelGGL(k_symv, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, U, dim, x, partial, parity);
+  if (cnt)
+    hipLaunchKernelGGL(k_symv<true>, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, U, dim, x, partial, parity, cnt, y);
+  else
+    hipLaunchKernelGGL(k_symv<false>, dim3(nb * (nb + 1) / 2), dim3(256), 0, st, U, dim, x, partial, parity,
+                       cnt, y);
   return hipGetLastError();
 }
 

@@ -206,6 +206,10 @@ struct dse_ctx {
   // holds 256 MiB of U) and released by dse_destroy or when a larger register needs more
   unsigned char* d_mx = nullptr;
   size_t mx_cap = 0;
+  // option "symv_fused": each product's reduction inside the product's launch (agent-scope counters
+  // with a release per workgroup): measured 22.9 vs 10.4 ms for config 2, so off by default
+  int symv_fused = 0;
+
   hipStream_t dense_stream = nullptr;
   rocblas_handle blas = nullptr;
 };
@@ -1203,6 +1207,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "matrix") {  // propagator-matrix mode: 0 off, 1 auto, 2 always (when eligible)
     if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "matrix must be 0, 1 or 2");
     ctx->matrix = (int)value;
+  } else if (k == "symv_fused") {  // matrix mode: each product's reduction in the product's launch
+    ctx->symv_fused = value != 0.0;
   } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
     if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "dense must be 0, 1 or 2");
     ctx->dense = (int)value;
@@ -1837,8 +1843,11 @@ bool matrix_eligible(const HostProblem& P, const double* t, int n_t, double* dt_
 }
 
 // seconds: the chain on one workgroup (~11.4 us per term at 2^12 amplitudes, linear in the tile)
-// against the column build spread over the chip (2 workgroups per CU below 2^13) plus n_t - 1
-// matrix-vector products at ~5 TB/s
+// against the column build spread over the chip plus n_t - 1 matrix-vector products.  Real build
+// (k_ucols, imaginary or real drives): ~10 us per term and workgroup at 2^12 amplitudes with two
+// workgroups per CU (one at 2^13, LDS), products over the half matrix at ~5 TB/s plus ~5 us for the
+// reduction launch; complex build (k_interval column mode): as the chain's terms, two workgroups
+// per CU below 2^13, products over the whole matrix (zgemv) at ~3 TB/s.
 bool matrix_cheaper(const HostProblem& P, double dt, int n_t, int n_cu) {
   const double dim = std::ldexp(1.0, P.n_local);
   const double alpha = 0.5 * (P.e_max - P.e_min);
@@ -1846,9 +1855,11 @@ bool matrix_cheaper(const HostProblem& P, double dt, int n_t, int n_cu) {
   const double deg1 = z + 12.0 * std::cbrt(z + 1.0) + 20.0;
   const double t_term = 11.4e-6 * std::max(dim / 4096.0, 0.25);
   const double chain = (n_t - 1) * deg1 * t_term;
+  const bool real = dense_eligible(P) && ucols_supported(P.L) && P.n_local == P.L;
   const double slots = (double)n_cu * (P.L < 13 ? 2.0 : 1.0);
-  const double build = std::ceil(dim / slots) * deg1 * t_term;
-  const double chain_u = (n_t - 1) * dim * dim * 16.0 / 5e12;
+  const double t_col = real ? 10e-6 * std::max(dim / 4096.0, 0.25) : t_term;
+  const double build = std::ceil(dim / slots) * deg1 * t_col;
+  const double chain_u = (n_t - 1) * (real ? dim * dim * 8.0 / 5e12 + 5e-6 : dim * dim * 16.0 / 3e12);
   return build + chain_u < chain;
 }
 
@@ -1898,7 +1909,8 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
   const size_t oU = take(u_elems * sizeof(double2)), oS = take(dim * (size_t)n_t * sizeof(double2)),
                oPart = take(real_build ? nb * dim * sizeof(double2) : 0), oObs = take((size_t)n_t * 8 * sizeof(double)),
                oDesc = take(sizeof(DenseProb)), oProb = take(sizeof(DevProb)),
-               oCoef = take(std::max(row.size() * sizeof(double2), cf.size() * sizeof(double))), oErr = take(sizeof(int));
+               oCoef = take(std::max(row.size() * sizeof(double2), cf.size() * sizeof(double))), oErr = take(sizeof(int)),
+               oCnt = take(nb * sizeof(int));
   if (off > ctx->mx_cap) {
     if (ctx->d_mx) (void)hipFree(ctx->d_mx), ctx->d_mx = nullptr;
     ctx->mx_cap = 0;
@@ -1913,11 +1925,13 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
   DenseProb* d_desc = reinterpret_cast<DenseProb*>(base + oDesc);
   DevProb* d_p = reinterpret_cast<DevProb*>(base + oProb);
   int* d_err = reinterpret_cast<int*>(base + oErr);
+  int* d_cnt = reinterpret_cast<int*>(base + oCnt);
   DevProb d = ctx->h_desc[pi];
   d.beta = beta;
   d.s1 = 1.0 / alpha;
   d.degree = deg;
   HIPC(hipMemsetAsync(d_err, 0, sizeof(int), st));
+  HIPC(hipMemsetAsync(d_cnt, 0, nb * sizeof(int), st));
   DevArena ar;  // complex build only: the basis columns
   if (real_build) {
     double* d_cf = reinterpret_cast<double*>(base + oCoef);
@@ -1965,8 +1979,12 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
     HIPC(hipMemcpyAsync(S + dim, U + P.psi0 * dim, dim * sizeof(double2), hipMemcpyDeviceToDevice, st));
   const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
   for (int j = 1; j + 1 < n_t && real_build; ++j) {
-    HIPC(launch_symv(U, (int)dim, S + dim * j, part, P.imag ? 1 : 0, st));
-    HIPC(launch_symv_reduce(part, (int)dim, S + dim * (j + 1), st));
+    if (ctx->symv_fused) {
+      HIPC(launch_symv(U, (int)dim, S + dim * j, part, P.imag ? 1 : 0, st, d_cnt, S + dim * (j + 1)));
+    } else {
+      HIPC(launch_symv(U, (int)dim, S + dim * j, part, P.imag ? 1 : 0, st));
+      HIPC(launch_symv_reduce(part, (int)dim, S + dim * (j + 1), st));
+    }
   }
   for (int j = 1; j + 1 < n_t && !real_build; ++j) {
     const rocblas_status rs = rocblas_zgemv(ctx->blas, rocblas_operation_none, (rocblas_int)dim, (rocblas_int)dim,

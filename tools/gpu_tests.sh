@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU test pass: the whole -m gpu suite (or the files given), one process, per-test timeout.
+# GPU test suite alone (tag argument names the output directory).
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "${@:-tests}" \
-  > gpurun_out/gpu_tests.log 2>&1
-rc=$?
-tail -5 gpurun_out/gpu_tests.log
+OUT=gpurun_out/r03/${1:-tests}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests > $OUT/gpu_tests.log 2>&1; rc=$?
+tail -4 $OUT/gpu_tests.log
 exit $rc
