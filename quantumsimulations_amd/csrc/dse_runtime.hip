@@ -138,6 +138,7 @@ struct dse_ctx {
   int wht = 1;                      // Walsh-Hadamard engine for registers of more tiles
   int wht_group_bits = 0;           // high bits per pass of that engine (0: tile bits - 2)
   int wht_tile_bits = 0;            // its tile: 12, 13 (0 = 13)
+  int wht_persist = 0;              // bit 1: MID as a persistent launch (k_wht_mid_p), option wht_persist
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
@@ -908,7 +909,8 @@ int wht_run(dse_ctx* ctx, int wl, int G, const std::vector<std::pair<const int2*
   int rc;
   auto part = [&](int pt, int vsel) -> int {
     for (const auto& sg : segs)
-      HIPC(launch_wht_part(pt, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, vsel, st));
+      HIPC(launch_wht_part(pt, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, vsel, st,
+                           ctx->n_cu * (wl == 13 ? 1 : 2), ctx->wht_persist));
     return DSE_OK;
   };
   if (regs.empty() || !ctx->swap_overlap) {
@@ -1176,6 +1178,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
       free_device(ctx);
       ctx->wht = value != 0.0;
     }
+  } else if (k == "wht_persist") {  // Walsh-Hadamard passes as persistent launches: bit 1 MID
+    ctx->wht_persist = (int)value;
   } else if (k == "wht_tile_bits") {
     if (!(value == 0 || value == 12 || value == 13)) return fail(ctx, DSE_ERR_ARG, "wht_tile_bits must be 0, 12 or 13");
     if ((int)value != ctx->wht_tile_bits) {

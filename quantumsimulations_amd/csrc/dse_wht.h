@@ -64,7 +64,9 @@ hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64
 // vsel 1 = FIRST + FWD(A), 2 = FWD(B); mid = MID(vsel); post with vsel 1 = INV(A), 2 = INV(B) +
 // FINAL -- so a partitioned register can swap one vector while the other is transformed.
 enum { WHT_PART_PRE = 0, WHT_PART_MID = 1, WHT_PART_POST = 2 };
+// pgrid > 0 with pmask bit 1: MID as a persistent launch of pgrid workgroups (k_wht_mid_p)
 hipError_t launch_wht_part(int part, int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
-                           const int2* items, int n_items, int k, int q, int set, int vsel, hipStream_t st);
+                           const int2* items, int n_items, int k, int q, int set, int vsel, hipStream_t st,
+                           int pgrid = 0, int pmask = 0);
 
 }  // namespace dse

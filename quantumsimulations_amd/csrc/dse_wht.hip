@@ -33,6 +33,8 @@
 // (2-way), and separable, slot = f(t) + g(r): one base address per thread, immediate offsets.
 // WL = 12 tiles (64 KiB) fit two workgroups per CU, so one workgroup's loads overlap the other's
 // transposes; WL = 13 needs fewer passes below 25 qubits.
+#include <algorithm>
+
 #include "dse_device.h"
 #include "dse_wht.h"
 
@@ -435,6 +437,99 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
   }
 }
 
+// Persistent MID (option wht_persist bit 1): gridDim.x workgroups loop over the items; a vector's
+// next tile is loaded as soon as its current tile is stored, so the loads of A(o + grid) land while
+// B(o) is transformed and those of B(o + grid) while A(o + grid) is -- one workgroup per CU keeps
+// HBM busy through its LDS transposes (the one-tile-per-workgroup form leaves them unoverlapped).
+template <int WL, int MODE, int VSEL>
+__global__ void __launch_bounds__(WG<WL>::NT)
+k_wht_mid_p(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, const int2* __restrict__ items,
+            int n_items, int g, int k) {
+  __shared__ WhtShared<WL> S;
+  const int tid = threadIdx.x;
+  int i = blockIdx.x;
+  if (i >= n_items) return;
+  auto lidx = [&](int item) {
+    const int2 it = items[item];
+    const WhtGroup& G = probs[it.x].grp[g];
+    return LayIdx<WL>(G, 0, tid, outer_bits(G, (uint64_t)(uint32_t)it.y));
+  };
+  double2 v[WR], vb[WR];
+  auto load_a = [&](int item) {
+    const LayIdx<WL> ia = lidx(item);
+    const gd2* XA = gptr((const double2*)probs[items[item].x].vec_at);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) v[r] = gld(XA, ia[r]);
+  };
+  auto load_b = [&](int item) {
+    const LayIdx<WL> ia = lidx(item);
+    const gd2* XB = gptr((const double2*)probs[items[item].x].vec_bt);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) vb[r] = gld(XB, ia[r]);
+  };
+  if constexpr ((VSEL & 1) != 0) load_a(i);
+  if constexpr ((VSEL & 2) != 0) load_b(i);
+  for (; i < n_items; i += gridDim.x) {
+    const int2 it = items[i];
+    const WhtProb& W = probs[it.x];
+    const int inext = i + (int)gridDim.x;
+    // a problem whose series has ended (k past its degree) is transformed but not stored: one code
+    // path, so the next tile's loads stay where they are
+    const bool live = !(MODE == MODE_GEN && k > dprobs[it.x].degree);
+    const WhtGroup& G = W.grp[g];
+    const uint64_t o = (uint64_t)(uint32_t)it.y;
+    const int last = has_b<WL>(G.c) ? 1 : 0;
+    const LayIdx<WL> ia(G, 0, tid, outer_bits(G, o));
+    // S.f of this tile: the previous tile's last reads of S.f came before its back transforms,
+    // whose transposes hold workgroup barriers
+    if (tid < 32) {
+      const double c = gptr((const double*)W.xytab)[o * 32 + tid];
+      if (tid <= WL) S.f[0][tid] = c;
+      else if (tid >= 16 && tid <= 16 + WL) S.f[1][tid - 16] = c;
+    }
+    double qt, qh[4];
+    pair_parts<WL>(W.qtab, tid, qt, qh);
+    const double* zr = W.qtab + 5 * WG<WL>::NT;
+    __syncthreads();  // S.f
+    auto diag = [&](double2* x, int vec) {
+      const double sg = vec == 0 ? 1.0 : -1.0;
+      double lt, lh[4];
+      lin_parts<WL>(S.f[vec], last, tid, lt, lh);
+      lt += sg * qt;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lh[q] += sg * qh[q];
+#pragma unroll
+      for (int r = 0; r < WR; ++r) {
+        const double d = quad_at(lt, lh, zr[r], sg, r);
+        x[r].x *= d;
+        x[r].y *= d;
+      }
+    };
+    if constexpr ((VSEL & 1) != 0) {
+      gd2* XA = gptr(W.vec_at);
+      tile_fwd<WL>(S.w, v, G.c, tid);
+      diag(v, 0);
+      tile_back<WL>(S.w, v, G.c, last, tid);
+      if (live) {
+#pragma unroll
+        for (int r = 0; r < WR; ++r) gst(XA, ia[r], v[r]);
+      }
+      if (inext < n_items) load_a(inext);
+    }
+    if constexpr ((VSEL & 2) != 0) {
+      gd2* XB = gptr(W.vec_bt);
+      tile_fwd<WL>(S.w, vb, G.c, tid);
+      diag(vb, 1);
+      tile_back<WL>(S.w, vb, G.c, last, tid);
+      if (live) {
+#pragma unroll
+        for (int r = 0; r < WR; ++r) gst(XB, ia[r], vb[r]);
+      }
+      if (inext < n_items) load_b(inext);
+    }
+  }
+}
+
 // One thread per tile o: D_Z pieces of group-0 tile o (tile_diag_coeffs without beta) and the
 // D_X / D_Y pieces of MID-group tile o:  F_q = lin(pos_q) + sum_i c(pos_q, opos_i) z_i,
 // C = sum_i lin(opos_i) z_i + sum_{i<j} c(opos_i, opos_j) z_i z_j  (D_Y: lin_y, -c).
@@ -562,10 +657,29 @@ hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int
   }
 }
 
+template <int WL, int VSEL>
+hipError_t launch_mid_p(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items, int g,
+                        int k, int grid, hipStream_t st) {
+  const dim3 gr(std::min(grid, n_items)), block(WG<WL>::NT);
+  if (mode == MODE_APPLY)
+    hipLaunchKernelGGL((k_wht_mid_p<WL, MODE_APPLY, VSEL>), gr, block, 0, st, wp, dp, items, n_items, g, k);
+  else if (mode == MODE_FIRST)
+    hipLaunchKernelGGL((k_wht_mid_p<WL, MODE_FIRST, VSEL>), gr, block, 0, st, wp, dp, items, n_items, g, k);
+  else
+    hipLaunchKernelGGL((k_wht_mid_p<WL, MODE_GEN, VSEL>), gr, block, 0, st, wp, dp, items, n_items, g, k);
+  return hipGetLastError();
+}
+
 template <int WL>
 hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const DevProb* dp, const int2* items,
-                    int n_items, int k, int q, int set, int vsel, hipStream_t st) {
+                    int n_items, int k, int q, int set, int vsel, hipStream_t st, int pgrid, int pmask) {
   hipError_t e = hipSuccess;
+  if (part == WHT_PART_MID && pgrid > 0 && (pmask & 2)) {  // persistent MID
+    const int g = n_groups - 1;
+    if (vsel == 3) return launch_mid_p<WL, 3>(mode, wp, dp, items, n_items, g, k, pgrid, st);
+    if (vsel == 1) return launch_mid_p<WL, 1>(mode, wp, dp, items, n_items, g, k, pgrid, st);
+    return launch_mid_p<WL, 2>(mode, wp, dp, items, n_items, g, k, pgrid, st);
+  }
   if (part == WHT_PART_PRE) {
     if (vsel & 1) e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
     for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
@@ -598,11 +712,12 @@ hipError_t launch_wht_tables(int wl, const WhtProb* wp, const DevProb* dp, int64
 }
 
 hipError_t launch_wht_part(int part, int wl, int mode, int n_groups, const WhtProb* wp, const DevProb* dp,
-                           const int2* items, int n_items, int k, int q, int set, int vsel, hipStream_t st) {
+                           const int2* items, int n_items, int k, int q, int set, int vsel, hipStream_t st,
+                           int pgrid, int pmask) {
   if (n_items <= 0) return hipSuccess;
   if (n_groups < 2 || n_groups > kWhtMaxGroups || vsel < 1 || vsel > 3) return hipErrorInvalidValue;
-  if (wl == 12) return wht_part<12>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, vsel, st);
-  if (wl == 13) return wht_part<13>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, vsel, st);
+  if (wl == 12) return wht_part<12>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, vsel, st, pgrid, pmask);
+  if (wl == 13) return wht_part<13>(part, mode, n_groups, wp, dp, items, n_items, k, q, set, vsel, st, pgrid, pmask);
   return hipErrorInvalidValue;
 }
 

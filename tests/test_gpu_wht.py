@@ -221,3 +221,30 @@ def test_wht_swap_overlap_is_schedule_independent(engine, n, bits):
         engine.set_option("swap_overlap", 1)
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("n,tile_bits,shard_bits", [(22, 13, 0), (21, 12, 0), (20, 13, 2)])
+def test_wht_persistent_mid_is_bitwise_identical(engine, n, tile_bits, shard_bits):
+    """Option wht_persist bit 1: MID as a persistent launch (k_wht_mid_p: each workgroup loops over
+    tiles, a vector's next tile loaded while the other vector is transformed) does the same
+    arithmetic per tile as one workgroup per tile, so results agree bit for bit -- whole and
+    partitioned registers, both tile sizes."""
+    prob = _random_problem(n, 2200 + n, rare_bit=n - 1)
+    t = np.linspace(0.0, 2e-4, 4)
+    out = {}
+    try:
+        engine.set_option("wht_tile_bits", tile_bits)
+        for pm in (0, 2):
+            engine.clear()
+            engine.set_option("wht_persist", pm)
+            ps = engine.add_sharded(prob, shard_bits) if shard_bits else engine.add(prob)
+            obs, st = engine.evolve(t)
+            assert st["mode"] == 2
+            k = 1 << shard_bits
+            out[pm] = (obs[ps:ps + k].copy(), engine.state(ps))
+    finally:
+        engine.clear()
+        engine.set_option("wht_persist", 0)
+        engine.set_option("wht_tile_bits", 0)
+    assert np.array_equal(out[0][0], out[2][0])
+    assert np.array_equal(out[0][1], out[2][1])
