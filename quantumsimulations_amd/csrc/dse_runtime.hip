@@ -25,6 +25,8 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <memory>
+#include <atomic>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -213,6 +215,12 @@ struct dse_ctx {
 
   hipStream_t dense_stream = nullptr;
   rocblas_handle blas = nullptr;
+  // dense engine: registers of >= 2^10 amplitudes are diagonalised up to eig_streams at a time (one
+  // host thread, stream and rocBLAS handle each; option "eig_streams", default 2: measured 0.88 of
+  // the one-by-one time per solve at 2^14, 0.81 at 2^13, profiles/r03/eig_concurrency_*.jsonl)
+  int eig_streams = 2;
+  std::vector<hipStream_t> eig_st;
+  std::vector<rocblas_handle> eig_h;
 };
 
 namespace {
@@ -346,6 +354,10 @@ void destroy_lanes(dse_ctx* ctx) {
     ctx->small_stream = nullptr;
   }
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas), ctx->blas = nullptr;
+  for (auto& h : ctx->eig_h) (void)rocblas_destroy_handle(h);
+  ctx->eig_h.clear();
+  for (auto& e : ctx->eig_st) (void)hipStreamSynchronize(e), (void)hipStreamDestroy(e);
+  ctx->eig_st.clear();
   for (auto e : ctx->xev) (void)hipEventDestroy(e);
   ctx->xev.clear();
   ctx->xev_used = 0;
@@ -1211,6 +1223,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "matrix") {  // propagator-matrix mode: 0 off, 1 auto, 2 always (when eligible)
     if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "matrix must be 0, 1 or 2");
     ctx->matrix = (int)value;
+  } else if (k == "eig_streams") {  // dense engine: large eigendecompositions at a time (1..8)
+    if (!(value >= 1 && value <= 8)) return fail(ctx, DSE_ERR_ARG, "eig_streams must be in 1..8");
+    ctx->eig_streams = (int)value;
   } else if (k == "symv_fused") {  // matrix mode: each product's reduction in the product's launch
     ctx->symv_fused = value != 0.0;
   } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
@@ -1698,13 +1713,31 @@ struct DevArena {  // device allocations of one dense_run, freed on every exit p
 };
 
 // Every problem with P.dn: H' built on the device, diagonalised (rocSOLVER dsyevd, batched for
-// registers of equal size), outputs in blocks of TB times as Psi' = V [cos | -sin] (rocBLAS
-// dgemm_strided_batched), observables and the final state from Psi'.  Blocking; writes obs_out.
+// registers of equal size below 2^10 amplitudes, one call per register above), outputs in blocks of
+// TB times as Psi' = V [cos | -sin] (rocBLAS dgemm_strided_batched), observables and the final
+// state from Psi'.  Work proceeds in rounds that fit 60% of the free device memory: every job
+// (registers of one size) of a round is built, then all its eigendecompositions run on up to
+// eig_streams solver streams at once (largest first, across sizes), then the output GEMMs.
+// Blocking; writes obs_out.
+struct DenseJob {
+  int n = 0, cnt = 0, TB = 1;
+  size_t dim = 0, pstride = 0;
+  std::vector<int> list;  // problem indices
+  DevArena ba;
+  double *V = nullptr, *lam = nullptr, *E = nullptr, *Pm = nullptr, *Psi = nullptr, *obs = nullptr;
+  rocblas_int* info = nullptr;
+  DenseProb* d_desc = nullptr;
+};
+
 int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* ms_all, double* ms_eig) {
-  std::map<int, std::vector<int>> by_n;
-  for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
-    if (ctx->probs[pi].dn) by_n[ctx->probs[pi].n_local].push_back((int)pi);
-  if (by_n.empty()) return DSE_OK;
+  std::vector<int> order;  // dense problems, by register size
+  {
+    std::map<int, std::vector<int>> by_n;
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi)
+      if (ctx->probs[pi].dn) by_n[ctx->probs[pi].n_local].push_back((int)pi);
+    for (auto& kv : by_n) order.insert(order.end(), kv.second.begin(), kv.second.end());
+  }
+  if (order.empty()) return DSE_OK;
   const auto c0 = std::chrono::steady_clock::now();
   double eig_ms = 0.0;
   if (!ctx->dense_stream) HIPC(hipStreamCreateWithFlags(&ctx->dense_stream, hipStreamNonBlocking));
@@ -1719,36 +1752,48 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
   double* d_tau = arena.get<double>(n_t);
   if (!d_tau) return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed");
   HIPC(hipMemcpyAsync(d_tau, tau.data(), n_t * sizeof(double), hipMemcpyHostToDevice, st));
-  for (auto& kv : by_n) {
-    const int n = kv.first;
-    const std::vector<int>& list = kv.second;
-    const size_t dim = size_t(1) << n;
-    // outputs per block: P and Psi' of a problem take 2 x dim x 2 TB doubles (<= 256 MiB each)
-    const int TB = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_t, (size_t(256) << 20) / (16 * dim)));
-    const size_t pstride = dim * 2 * (size_t)TB;
+  size_t idx = 0;
+  while (idx < order.size()) {
+    // ---- round: jobs while 60% of the free memory lasts (at least one register) ----
     size_t free_b = 0, total_b = 0;
     HIPC(hipMemGetInfo(&free_b, &total_b));
-    const size_t per = (dim * dim + 2 * pstride + 3 * dim + (size_t)n_t * 8 + 2 * n * n + 4 * n) * sizeof(double);
-    const size_t B = std::max<size_t>(1, std::min<size_t>(list.size(), (size_t)(0.6 * (double)free_b) / per));
-    for (size_t b0 = 0; b0 < list.size(); b0 += B) {
-      const int cnt = (int)std::min(B, list.size() - b0);
-      DevArena ba;
-      double* V = ba.get<double>(dim * dim * cnt);
-      double* lam = ba.get<double>(dim * cnt);
-      double* E = ba.get<double>(dim * cnt);
-      rocblas_int* info = ba.get<rocblas_int>(cnt);
-      double* Pm = ba.get<double>(pstride * cnt);
-      double* Psi = ba.get<double>(pstride * cnt);
-      double* obs = ba.get<double>((size_t)n_t * 8 * cnt);
+    const double budget = 0.6 * (double)free_b;
+    double used = 0.0;
+    std::vector<std::unique_ptr<DenseJob>> jobs;
+    while (idx < order.size()) {
+      const int n = ctx->probs[order[idx]].n_local;
+      const size_t dim = size_t(1) << n;
+      // outputs per block: P and Psi' of a problem take 2 x dim x 2 TB doubles (<= 256 MiB each)
+      const int TB = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_t, (size_t(256) << 20) / (16 * dim)));
+      const size_t pstride = dim * 2 * (size_t)TB;
+      const double per = (double)((dim * dim + 2 * pstride + 3 * dim + (size_t)n_t * 8 + 2 * n * n + 4 * n) * sizeof(double));
+      size_t same = 0;
+      while (idx + same < order.size() && ctx->probs[order[idx + same]].n_local == n) ++same;
+      size_t cnt = (size_t)std::max(0.0, (budget - used) / per);
+      if (cnt == 0 && !jobs.empty()) break;
+      cnt = std::max<size_t>(1, std::min(cnt, same));
+      auto J = std::make_unique<DenseJob>();
+      J->n = n, J->dim = dim, J->TB = TB, J->pstride = pstride, J->cnt = (int)cnt;
+      J->list.assign(order.begin() + idx, order.begin() + idx + cnt);
+      DevArena& ba = J->ba;
+      J->V = ba.get<double>(dim * dim * cnt);
+      J->lam = ba.get<double>(dim * cnt);
+      J->E = ba.get<double>(dim * cnt);
+      J->info = ba.get<rocblas_int>(cnt);
+      J->Pm = ba.get<double>(pstride * cnt);
+      J->Psi = ba.get<double>(pstride * cnt);
+      J->obs = ba.get<double>((size_t)n_t * 8 * cnt);
       const size_t tsz = (size_t)(2 * n * n + 5 * n);
       double* tabs = ba.get<double>(tsz * cnt);
-      DenseProb* d_desc = ba.get<DenseProb>(cnt);
-      if (!V || !lam || !E || !info || !Pm || !Psi || !obs || !tabs || !d_desc)
+      J->d_desc = ba.get<DenseProb>(cnt);
+      if (!J->V || !J->lam || !J->E || !J->info || !J->Pm || !J->Psi || !J->obs || !tabs || !J->d_desc) {
+        if (!jobs.empty()) break;  // this round is full: the register waits for the next one
         return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed (dim " + std::to_string(dim) + ")");
+      }
       std::vector<double> htabs(tsz * cnt, 0.0);
       std::vector<DenseProb> desc(cnt);
-      for (int i = 0; i < cnt; ++i) {
-        const HostProblem& P = ctx->probs[list[b0 + i]];
+      for (size_t i = 0; i < cnt; ++i) {
+        const HostProblem& P = ctx->probs[J->list[i]];
         double* h = htabs.data() + tsz * i;
         std::copy(P.field.begin(), P.field.begin() + n, h);
         std::copy(P.zz.begin(), P.zz.begin() + n * n, h + n);
@@ -1767,33 +1812,90 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         D.zz = d + n;
         D.pair = d + n + n * n;
         D.flip = d + n + 2 * n * n;
-        D.V = V + dim * dim * i;
-        D.lam = lam + dim * i;
-        D.obs = obs + (size_t)n_t * 8 * i;
+        D.V = J->V + dim * dim * i;
+        D.lam = J->lam + dim * i;
+        D.obs = J->obs + (size_t)n_t * 8 * i;
         D.final_state = P.buf[0];
       }
       HIPC(hipMemcpyAsync(tabs, htabs.data(), htabs.size() * sizeof(double), hipMemcpyHostToDevice, st));
-      HIPC(hipMemcpyAsync(d_desc, desc.data(), desc.size() * sizeof(DenseProb), hipMemcpyHostToDevice, st));
-      HIPC(hipMemsetAsync(V, 0, dim * dim * cnt * sizeof(double), st));
-      HIPC(launch_dense_h(d_desc, cnt, (int)dim, st));
-      HIPC(hipStreamSynchronize(st));
-      const auto e0 = std::chrono::steady_clock::now();
-      rocblas_status rs = rocblas_status_success;
-      if (dim >= 1024) {  // large registers one by one (the batched solver targets small matrices)
-        for (int i = 0; i < cnt && rs == rocblas_status_success; ++i)
-          rs = rocsolver_dsyevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, (rocblas_int)dim,
-                                V + dim * dim * i, (rocblas_int)dim, lam + dim * i, E + dim * i, info + i);
-      } else {
-        rs = rocsolver_dsyevd_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper,
-                                              (rocblas_int)dim, V, (rocblas_int)dim, (rocblas_stride)(dim * dim),
-                                              lam, (rocblas_stride)dim, E, (rocblas_stride)dim, info, cnt);
+      HIPC(hipMemcpyAsync(J->d_desc, desc.data(), desc.size() * sizeof(DenseProb), hipMemcpyHostToDevice, st));
+      HIPC(hipMemsetAsync(J->V, 0, dim * dim * cnt * sizeof(double), st));
+      HIPC(launch_dense_h(J->d_desc, (int)cnt, (int)dim, st));
+      HIPC(hipStreamSynchronize(st));  // the host tables may go
+      used += per * (double)cnt;
+      idx += cnt;
+      jobs.push_back(std::move(J));
+    }
+    // ---- the round's eigendecompositions: one task per large register, one batched task per job of
+    // small ones, largest first, over up to eig_streams solver streams ----
+    const auto e0 = std::chrono::steady_clock::now();
+    struct Task {
+      DenseJob* j;
+      int i;  // register within the job; -1: the whole job, batched
+    };
+    std::vector<Task> tasks;
+    for (auto& J : jobs) {
+      if (J->dim >= 1024)
+        for (int i = 0; i < J->cnt; ++i) tasks.push_back({J.get(), i});
+      else
+        tasks.push_back({J.get(), -1});
+    }
+    std::stable_sort(tasks.begin(), tasks.end(), [](const Task& x, const Task& y) { return x.j->dim > y.j->dim; });
+    const int K = std::max(1, std::min(ctx->eig_streams, (int)tasks.size()));
+    while ((int)ctx->eig_h.size() < K) {
+      hipStream_t es = nullptr;
+      rocblas_handle eh = nullptr;
+      HIPC(hipStreamCreateWithFlags(&es, hipStreamNonBlocking));
+      if (rocblas_create_handle(&eh) != rocblas_status_success || rocblas_set_stream(eh, es) != rocblas_status_success) {
+        if (eh) (void)rocblas_destroy_handle(eh);
+        (void)hipStreamDestroy(es);
+        return fail(ctx, DSE_ERR_HIP, "rocblas handle for the eigensolver streams failed");
       }
-      if (rs != rocblas_status_success)
-        return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)rs) + ")");
+      ctx->eig_st.push_back(es);
+      ctx->eig_h.push_back(eh);
+    }
+    std::atomic<size_t> next{0};
+    std::vector<rocblas_status> wst(K, rocblas_status_success);
+    std::vector<hipError_t> werr(K, hipSuccess);
+    auto worker = [&](int w) {
+      for (size_t ti = next++; ti < tasks.size() && wst[w] == rocblas_status_success; ti = next++) {
+        const Task& T = tasks[ti];
+        DenseJob& J = *T.j;
+        const rocblas_int dim = (rocblas_int)J.dim;
+        if (T.i >= 0) {
+          const size_t i = (size_t)T.i;
+          wst[w] = rocsolver_dsyevd(ctx->eig_h[w], rocblas_evect_original, rocblas_fill_upper, dim,
+                                    J.V + J.dim * J.dim * i, dim, J.lam + J.dim * i, J.E + J.dim * i, J.info + i);
+        } else {
+          wst[w] = rocsolver_dsyevd_strided_batched(ctx->eig_h[w], rocblas_evect_original, rocblas_fill_upper, dim,
+                                                    J.V, dim, (rocblas_stride)(J.dim * J.dim), J.lam,
+                                                    (rocblas_stride)J.dim, J.E, (rocblas_stride)J.dim, J.info, J.cnt);
+        }
+      }
+      werr[w] = hipStreamSynchronize(ctx->eig_st[w]);
+    };
+    if (K == 1) {
+      worker(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int w = 0; w < K; ++w) th.emplace_back(worker, w);
+      for (auto& x : th) x.join();
+    }
+    for (int w = 0; w < K; ++w) {
+      if (werr[w] != hipSuccess)
+        return fail(ctx, DSE_ERR_HIP, std::string("eigensolver stream: ") + hipGetErrorString(werr[w]));
+      if (wst[w] != rocblas_status_success)
+        return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)wst[w]) + ")");
+    }
+    eig_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e0).count();
+    // ---- outputs of every job of the round ----
+    for (auto& Jp : jobs) {
+      DenseJob& J = *Jp;
+      const int cnt = J.cnt, TB = J.TB;
+      const size_t dim = J.dim, pstride = J.pstride;
       std::vector<rocblas_int> hinfo(cnt);
-      HIPC(hipMemcpyAsync(hinfo.data(), info, cnt * sizeof(rocblas_int), hipMemcpyDeviceToHost, st));
+      HIPC(hipMemcpyAsync(hinfo.data(), J.info, cnt * sizeof(rocblas_int), hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
-      eig_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e0).count();
       for (int i = 0; i < cnt; ++i)
         if (hinfo[i] != 0)
           return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: dsyevd did not converge (info " +
@@ -1801,22 +1903,21 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       const double one = 1.0, zero = 0.0;
       for (int tb0 = 0; tb0 < n_t; tb0 += TB) {
         const int tb = std::min(TB, n_t - tb0);
-        HIPC(launch_dense_phase(d_desc, cnt, (int)dim, d_tau + tb0, tb, Pm, pstride, st));
-        rs = rocblas_dgemm_strided_batched(ctx->blas, rocblas_operation_none, rocblas_operation_none,
-                                           (rocblas_int)dim, 2 * tb, (rocblas_int)dim, &one, V, (rocblas_int)dim,
-                                           (rocblas_stride)(dim * dim), Pm, (rocblas_int)dim,
-                                           (rocblas_stride)pstride, &zero, Psi, (rocblas_int)dim,
-                                           (rocblas_stride)pstride, cnt);
+        HIPC(launch_dense_phase(J.d_desc, cnt, (int)dim, d_tau + tb0, tb, J.Pm, pstride, st));
+        const rocblas_status rs = rocblas_dgemm_strided_batched(
+            ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)dim, 2 * tb, (rocblas_int)dim, &one,
+            J.V, (rocblas_int)dim, (rocblas_stride)(dim * dim), J.Pm, (rocblas_int)dim, (rocblas_stride)pstride, &zero,
+            J.Psi, (rocblas_int)dim, (rocblas_stride)pstride, cnt);
         if (rs != rocblas_status_success)
           return fail(ctx, DSE_ERR_HIP, "rocblas dgemm failed (status " + std::to_string((int)rs) + ")");
-        HIPC(launch_dense_obs(d_desc, cnt, (int)dim, Psi, pstride, tb, tb0, st));
-        if (tb0 + tb == n_t) HIPC(launch_dense_final(d_desc, cnt, (int)dim, Psi, pstride, tb, tau[n_t - 1], st));
+        HIPC(launch_dense_obs(J.d_desc, cnt, (int)dim, J.Psi, pstride, tb, tb0, st));
+        if (tb0 + tb == n_t) HIPC(launch_dense_final(J.d_desc, cnt, (int)dim, J.Psi, pstride, tb, tau[n_t - 1], st));
       }
       std::vector<double> h((size_t)n_t * 8 * cnt);
-      HIPC(hipMemcpyAsync(h.data(), obs, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPC(hipMemcpyAsync(h.data(), J.obs, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
       for (int i = 0; i < cnt; ++i) {
-        const int pi = list[b0 + i];
+        const int pi = J.list[i];
         for (int ti = 0; ti < n_t; ++ti)
           finish_obs(ctx->probs[pi], h.data() + ((size_t)i * n_t + ti) * 8,
                      obs_out + (size_t)pi * DSE_N_OBS * n_t + ti, (size_t)n_t);
