@@ -158,7 +158,18 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "handoff_fences"  persistent mode, 2-tile registers: 0 (default) the sc1 hand-off
  *                         (write-through payload, per-wave vmcnt(0) + barrier, sc1 flag and
  *                         poll); 1 adds an agent-scope release before every flag store and an
- *                         acquire after every poll */
+ *                         acquire after every poll
+ *          "wht_persist"  Walsh-Hadamard engine: bit 1 runs MID as a persistent launch (one
+ *                         workgroup per CU looping over tiles, next tile's loads under the other
+ *                         vector's transposes); 0 (default)
+ *          "dense"        dense eigen-propagator: 0 off, 1 by cost model (default), 2 always
+ *          "eig_streams"  dense engine: eigendecompositions of registers of >= 2^10 amplitudes
+ *                         run this many at a time, one stream and rocBLAS handle each, 1..8
+ *                         (default 2)
+ *          "matrix"       propagator-matrix mode for a lone register: 0 off, 1 by model
+ *                         (default), 2 whenever eligible
+ *          "symv_fused"   propagator-matrix mode: 1 sums each product's partials inside the
+ *                         product's launch (agent-scope counters); 0 (default) a second launch */
 int dse_set_option(dse_ctx* ctx, const char* key, double value);
 
 /* ---- problems ----------------------------------------------------------------------------- */
