@@ -539,6 +539,24 @@ def main():
     fpa = sum(flops_per_amp(p) * (1 << p.n_qubits) for p in probs) / sum(1 << p.n_qubits for p in probs)
     amp_terms = sum(s["timed_amp_terms"] for s in stats)       # their amplitudes x terms
     all_amp_terms = sum(s["amplitude_updates"] for s in stats)
+    def by_stream(stats):
+        # the same launches split by stream: lane 0 holds the 2-tile registers (the stream whose
+        # launches set the step time), the rest the 1-tile ones, whose launch durations include the
+        # time their workgroups wait for CUs held by lane 0's launch
+        l0_ms = sum(s_["lane0_kernel_ms"] for s_ in stats)
+        l0_n = sum(s_["lane0_launches"] for s_ in stats)
+        l0_amps = sum(s_["lane0_amp_terms"] for s_ in stats)
+        out = []
+        for name, ms, n, amps in (("lane 0 (2-tile registers)", l0_ms, l0_n, l0_amps),
+                                  ("other lanes (1-tile registers)", k_ms - l0_ms, k_launches - l0_n,
+                                   amp_terms - l0_amps)):
+            if n <= 0 or ms <= 0:
+                continue
+            gbs = 80.0 * amps / (ms * 1e-3) / 1e9
+            out.append({"stream": name, "launches": n, "avg_launch_us": ms / n * 1e3,
+                        "achieved": gbs, "frac": gbs / HBM_PEAK_GBS})
+        return out
+
     if mode == 1:
         # persistent interval kernel, priced as SURVEY.md §8(d) prices a fused Chebyshev term:
         # 80 B per amplitude (read w_{k-1}, w_{k-2}, acc; write w_k, acc) against the HBM peak
@@ -558,6 +576,7 @@ def main():
             "chip_level": {"achieved": 80.0 * all_amp_terms / dt / 1e9,
                            "frac": 80.0 * all_amp_terms / dt / 1e9 / HBM_PEAK_GBS,
                            "note": "all launches of the step (both streams overlap) / step wall time"},
+            "by_stream": by_stream(stats),
             "fp64": {"achieved_tflops": fp64, "peak_tflops": FP64_PEAK_TFLOPS,
                      "frac": fp64 / FP64_PEAK_TFLOPS if fp64 else None,
                      "algorithmic_flops_per_amp": fpa,

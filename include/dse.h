@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 7
+#define DSE_ABI_VERSION 8
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -103,6 +103,9 @@ typedef struct dse_stats {
   double exchange_ms;         /* partitioned registers over processes: time of the exchanges    */
                               /* (HIP events around each RCCL call on its stream; host wall     */
                               /* time of each host-transport exchange)                           */
+  double lane0_kernel_ms;     /* the timed launches of stream ("lane") 0 alone: summed HIP-event */
+  double lane0_launches;      /* time, their count and their amplitudes x terms -- in persistent */
+  double lane0_amp_terms;     /* mode lane 0 holds the 2-tile registers (the critical stream)    */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */

@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 7
+DSE_ABI_VERSION = 8
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -62,6 +62,9 @@ class DseStats(C.Structure):
         ("dense_ms", C.c_double),
         ("dense_eig_ms", C.c_double),
         ("exchange_ms", C.c_double),
+        ("lane0_kernel_ms", C.c_double),
+        ("lane0_launches", C.c_double),
+        ("lane0_amp_terms", C.c_double),
     ]
 
     def as_dict(self):

@@ -2693,6 +2693,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     }
 
   double step_ms = 0.0, launches_timed = 0.0, bytes_timed = 0.0, amps_timed = 0.0;
+  double lane0_ms = 0.0, lane0_launches = 0.0, lane0_amps = 0.0;  // lane 0 alone (stats)
   double launches = 0.0, amp_updates = 0.0, all_bytes = 0.0, all_flops = 0.0, flops_timed = 0.0;
   // per timed launch: algorithmic flops (pool_bytes), HBM bytes (pool_bytes2, streaming only) and
   // amplitude-terms (pool_amps: amplitudes x Chebyshev terms the launch computes)
@@ -2707,6 +2708,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       step_ms += ms;
       flops_timed += pool_bytes[li * 2 + pool][i];
       amps_timed += pool_amps[li * 2 + pool][i];
+      if (li == 0) lane0_ms += ms, lane0_amps += pool_amps[li * 2 + pool][i], lane0_launches += 1.0;
       if (i < pool_bytes2[li * 2 + pool].size()) bytes_timed += pool_bytes2[li * 2 + pool][i];
     }
     launches_timed += (double)ln.ev_used[pool];
@@ -2914,6 +2916,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->exchange_bytes = ctx->xbytes;
     if ((rc = xt_sum(ctx))) return rc;
     stats->exchange_ms = ctx->xms;
+    stats->lane0_kernel_ms = lane0_ms;
+    stats->lane0_launches = lane0_launches;
+    stats->lane0_amp_terms = lane0_amps;
   }
   return DSE_OK;
 }
