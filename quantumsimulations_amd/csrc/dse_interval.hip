@@ -368,18 +368,31 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
           for (int rr = 0; rr < NH; ++rr) rmad(u[(1 - hh) * NH + rr], g, ow[rr]);
         }
       }
-      // (thread bit j, top): applies iff t_j == b_pa, source t ^ e_j.  All nine thread bits in a
-      // software pipeline of 8-row halves (the next half in flight under the current FMAs), the
-      // coefficient zero in the lanes where the pair does not act
+      // (thread bit j, top): applies iff t_j == b_pa, source t ^ e_j.  Lane bits in a software
+      // pipeline of 8-row halves (the next half in flight under the current FMAs), the coefficient
+      // zero in the lanes where the pair does not act; thread bits j >= 6 index the wave, so the
+      // pair acts on a whole wave or not at all: those partner reads are skipped by a scalar branch
+      constexpr int JL = TB < 6 ? TB : 6;
       double2 ba[NH], bb[NH];
       ld_rows<NT, NH, NH>(S.w, tid ^ 1, 0, 0, ba);
 #pragma unroll
-      for (int j = 0; j < TB; ++j) {
+      for (int j = 0; j < JL; ++j) {
         const double gj = ((uint32_t)((tid >> j) & 1) == b_pa) ? S.xq[j] : 0.0;
         ld_rows<NT, NH, NH>(S.w, tid ^ (1 << j), 1, 0, bb);
 #pragma unroll
         for (int rr = 0; rr < NH; ++rr) rmad(u[rr], gj, ba[rr]);
-        if (j + 1 < TB) ld_rows<NT, NH, NH>(S.w, tid ^ (1 << (j + 1)), 0, 0, ba);
+        if (j + 1 < JL) ld_rows<NT, NH, NH>(S.w, tid ^ (1 << (j + 1)), 0, 0, ba);
+#pragma unroll
+        for (int rr = 0; rr < NH; ++rr) rmad(u[NH + rr], gj, bb[rr]);
+      }
+#pragma unroll
+      for (int j = JL; j < TB; ++j) {
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((tid >> j) & 1) != b_pa) continue;  // whole wave
+        const double gj = S.xq[j];
+        ld_rows<NT, NH, NH>(S.w, tid ^ (1 << j), 0, 0, ba);
+        ld_rows<NT, NH, NH>(S.w, tid ^ (1 << j), 1, 0, bb);
+#pragma unroll
+        for (int rr = 0; rr < NH; ++rr) rmad(u[rr], gj, ba[rr]);
 #pragma unroll
         for (int rr = 0; rr < NH; ++rr) rmad(u[NH + rr], gj, bb[rr]);
       }

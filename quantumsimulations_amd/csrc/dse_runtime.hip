@@ -24,10 +24,15 @@
 #include <map>
 #include <numeric>
 #include <string>
-#include <thread>
-#include <memory>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include <rccl/rccl.h>
 #include <rocblas/rocblas.h>
@@ -241,6 +246,68 @@ int fail(dse_ctx* c, int code, const std::string& msg) {
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Host worker threads kept for the process (created on first use, never joined: they only wait
+// on a condition variable between jobs), so a dse_evolve does not pay ~16 thread creations per
+// parallel section.  One job at a time; a caller that finds the pool busy (another context on
+// another host thread) runs its job on threads of its own instead.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();  // intentionally never destroyed (detached workers)
+    return *p;
+  }
+  size_t size() const { return workers_; }
+  // body(w) for w < nb, on the pool and the calling thread; false if the pool was busy
+  bool run(size_t nb, const std::function<void(size_t)>& body) {
+    if (getpid() != pid_) return false;  // a forked child has none of the workers
+    std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &body;
+      nb_ = nb;
+      next_.store(0);
+      active_ = workers_;
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return active_ == 0; });
+    job_ = nullptr;
+    return true;
+  }
+
+ private:
+  HostPool() : workers_(std::min<size_t>(15, std::max(1u, std::thread::hardware_concurrency()) - 1)), pid_(getpid()) {
+    for (size_t w = 0; w < workers_; ++w) std::thread([this] { loop(); }).detach();
+  }
+  void drain() {
+    for (size_t b = next_++; b < nb_; b = next_++) (*job_)(b);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      drain();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--active_ == 0) done_.notify_all();
+    }
+  }
+  const size_t workers_;
+  const pid_t pid_;
+  std::mutex busy_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  size_t nb_ = 0, active_ = 0;
+  uint64_t gen_ = 0;
+  std::atomic<size_t> next_{0};
+};
+
 // f(i) for i < n on up to 16 host threads (contiguous blocks; f must touch only item i's data).
 template <class F>
 void parallel_for(size_t n, F&& f) {
@@ -249,12 +316,13 @@ void parallel_for(size_t n, F&& f) {
     for (size_t i = 0; i < n; ++i) f(i);
     return;
   }
+  const std::function<void(size_t)> block = [&](size_t w) {
+    for (size_t i = n * w / nth; i < n * (w + 1) / nth; ++i) f(i);
+  };
+  if (HostPool::get().run(nth, block)) return;
   std::vector<std::thread> th;
   th.reserve(nth);
-  for (size_t w = 0; w < nth; ++w)
-    th.emplace_back([&, w] {
-      for (size_t i = n * w / nth; i < n * (w + 1) / nth; ++i) f(i);
-    });
+  for (size_t w = 0; w < nth; ++w) th.emplace_back(block, w);
   for (auto& x : th) x.join();
 }
 
