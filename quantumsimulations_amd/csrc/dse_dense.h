@@ -59,6 +59,23 @@ hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const doub
 
 }  // namespace dse
 
+typedef struct _rocblas_handle* rocblas_handle;
+
+namespace dse {
+
+// ---- the half-matrix tridiagonalisation (dse_sytrd.hip): LAPACK dsytrd's lower layout (d, e, tau,
+// reflectors below the subdiagonal of A), the trailing-matrix products over the lower-triangle
+// tiles only.  work: sytrd_workspace(n) bytes.  0 on success.
+size_t sytrd_workspace(int n);
+int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* d, double* e, double* tau,
+                double* work);
+// A = V diag(lam) V^T (lower triangle of A read, A overwritten): sytrd_lower, rocsolver_dstedc,
+// rocsolver_dormtr.  e, tau: n doubles each; V: n x n, ldv >= n; info: rocsolver_dstedc's
+int eig_sym_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
+                  double* e, double* tau, double* work, int* info);
+
+}  // namespace dse
+
 namespace dse {
 
 // ---- propagator-matrix mode (dse_runtime.hip matrix_run): y = U x for the column-built

@@ -224,6 +224,11 @@ struct dse_ctx {
   // host thread, stream and rocBLAS handle each; option "eig_streams", default 2: measured 0.88 of
   // the one-by-one time per solve at 2^14, 0.81 at 2^13, profiles/r03/eig_concurrency_*.jsonl)
   int eig_streams = 2;
+  // dense engine eigensolver: 0 rocSOLVER dsyevd at every size; 1 the half-matrix tridiagonalisation
+  // (dse_sytrd.hip) + rocSOLVER dstedc / dormtr from kEigHalfMinDim amplitudes, dsyevd below
+  // (measured 3.03 vs 4.13 s at 2^14, 0.57 vs 0.68 s at 2^13, profiles/r03/sytrd_probe.jsonl);
+  // 2 the half-matrix path from 2^10 (tests)
+  int eig_impl = 1;
   std::vector<hipStream_t> eig_st;
   std::vector<rocblas_handle> eig_h;
 };
@@ -1294,6 +1299,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "eig_streams") {  // dense engine: large eigendecompositions at a time (1..8)
     if (!(value >= 1 && value <= 8)) return fail(ctx, DSE_ERR_ARG, "eig_streams must be in 1..8");
     ctx->eig_streams = (int)value;
+  } else if (k == "eig_impl") {  // dense engine eigensolver: 0 dsyevd, 1 auto, 2 half-matrix from 2^10
+    if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "eig_impl must be 0, 1 or 2");
+    ctx->eig_impl = (int)value;
   } else if (k == "symv_fused") {  // matrix mode: each product's reduction in the product's launch
     ctx->symv_fused = value != 0.0;
   } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
@@ -1787,6 +1795,9 @@ struct DevArena {  // device allocations of one dense_run, freed on every exit p
 // (registers of one size) of a round is built, then all its eigendecompositions run on up to
 // eig_streams solver streams at once (largest first, across sizes), then the output GEMMs.
 // Blocking; writes obs_out.
+// the half-matrix eigensolver's crossover (eig_impl 1): 0.57 vs 0.68 s at 2^13, slower at 2^12
+constexpr size_t kEigHalfMinDim = 8192;
+
 struct DenseJob {
   int n = 0, cnt = 0, TB = 1;
   size_t dim = 0, pstride = 0;
@@ -1820,6 +1831,12 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
   double* d_tau = arena.get<double>(n_t);
   if (!d_tau) return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed");
   HIPC(hipMemcpyAsync(d_tau, tau.data(), n_t * sizeof(double), hipMemcpyHostToDevice, st));
+  struct EigScratch {
+    double *A = nullptr, *tau = nullptr, *work = nullptr;
+  };
+  std::unique_ptr<DevArena> scr_arena;
+  std::vector<EigScratch> scr;
+  size_t scr_dim = 0;
   size_t idx = 0;
   while (idx < order.size()) {
     // ---- round: jobs while 60% of the free memory lasts (at least one register) ----
@@ -1922,15 +1939,52 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       ctx->eig_st.push_back(es);
       ctx->eig_h.push_back(eh);
     }
+    // half-matrix eigensolver scratch per solver stream: a copy of H' (the solver's A; V receives
+    // the eigenvectors), tau and the tridiagonalisation workspace, sized for the round's largest
+    // such register; kept across rounds
+    size_t half_min = ctx->eig_impl == 2 ? 1024 : ctx->eig_impl == 1 ? kEigHalfMinDim : SIZE_MAX;
+    size_t half_dim = 0;
+    for (const Task& T : tasks)
+      if (T.i >= 0 && T.j->dim >= half_min) half_dim = std::max(half_dim, T.j->dim);
+    if (half_dim > scr_dim) {
+      scr.clear();
+      scr_arena.reset(new DevArena);
+      scr_dim = 0;
+      for (int w = 0; w < K; ++w) {
+        EigScratch S;
+        S.A = scr_arena->get<double>(half_dim * half_dim);
+        S.tau = scr_arena->get<double>(half_dim);
+        S.work = scr_arena->get<double>(sytrd_workspace((int)half_dim) / sizeof(double) + 1);
+        if (!S.A || !S.tau || !S.work) break;
+        scr.push_back(S);
+      }
+      if ((int)scr.size() == K) {
+        scr_dim = half_dim;
+      } else {  // no room beside the round's jobs: dsyevd in place
+        (void)hipGetLastError();
+        scr.clear();
+        scr_arena.reset();
+        half_min = SIZE_MAX;
+      }
+    }
     std::atomic<size_t> next{0};
     std::vector<rocblas_status> wst(K, rocblas_status_success);
+    std::vector<int> wrc(K, 0);
     std::vector<hipError_t> werr(K, hipSuccess);
     auto worker = [&](int w) {
-      for (size_t ti = next++; ti < tasks.size() && wst[w] == rocblas_status_success; ti = next++) {
+      for (size_t ti = next++; ti < tasks.size() && wst[w] == rocblas_status_success && wrc[w] == 0; ti = next++) {
         const Task& T = tasks[ti];
         DenseJob& J = *T.j;
         const rocblas_int dim = (rocblas_int)J.dim;
-        if (T.i >= 0) {
+        if (T.i >= 0 && J.dim >= half_min) {
+          const size_t i = (size_t)T.i;
+          double* Vi = J.V + J.dim * J.dim * i;
+          werr[w] = hipMemcpyAsync(scr[w].A, Vi, J.dim * J.dim * sizeof(double), hipMemcpyDeviceToDevice,
+                                   ctx->eig_st[w]);
+          if (werr[w] != hipSuccess) break;
+          wrc[w] = eig_sym_lower(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
+                                 J.E + J.dim * i, scr[w].tau, scr[w].work, J.info + i);
+        } else if (T.i >= 0) {
           const size_t i = (size_t)T.i;
           wst[w] = rocsolver_dsyevd(ctx->eig_h[w], rocblas_evect_original, rocblas_fill_upper, dim,
                                     J.V + J.dim * J.dim * i, dim, J.lam + J.dim * i, J.E + J.dim * i, J.info + i);
@@ -1940,7 +1994,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
                                                     (rocblas_stride)J.dim, J.E, (rocblas_stride)J.dim, J.info, J.cnt);
         }
       }
-      werr[w] = hipStreamSynchronize(ctx->eig_st[w]);
+      const hipError_t se = hipStreamSynchronize(ctx->eig_st[w]);
+      if (werr[w] == hipSuccess) werr[w] = se;
     };
     if (K == 1) {
       worker(0);
@@ -1954,6 +2009,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         return fail(ctx, DSE_ERR_HIP, std::string("eigensolver stream: ") + hipGetErrorString(werr[w]));
       if (wst[w] != rocblas_status_success)
         return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)wst[w]) + ")");
+      if (wrc[w] != 0)
+        return fail(ctx, DSE_ERR_HIP, "half-matrix eigensolver failed (step " + std::to_string(-wrc[w]) + ")");
     }
     eig_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e0).count();
     // ---- outputs of every job of the round ----

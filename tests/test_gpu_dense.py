@@ -11,6 +11,9 @@ output time exact from one GEMM (rocBLAS dgemm) and the observable pass.
   sweep_sea_detuning.py:1223-1240) goes to the dense engine by the cost model (option dense = 1)
   and its first outputs agree with the Chebyshev engine on the same grid prefix; its norms stay 1
 * the cost model keeps the 1 ms N = 14 grid on the Chebyshev kernels
+* the half-matrix eigensolver (csrc/dse_sytrd.hip, option eig_impl): config 2 through it at dim 4096
+  against the exact fixture (1e-10) and against rocSOLVER dsyevd (1e-11); an N = 13 register (dim
+  8192, its default range) against dsyevd on a 1 s grid, to the phase drift of eigenvalue rounding
 """
 import numpy as np
 import pytest
@@ -23,9 +26,10 @@ pytestmark = pytest.mark.gpu
 OBS = rm.OBS_ORDER
 
 
-def _evolve(engine, params, t, dense):
+def _evolve(engine, params, t, dense, eig_impl=1):
     engine.clear()
     engine.set_option("dense", dense)
+    engine.set_option("eig_impl", eig_impl)
     try:
         for p in params:
             engine.add(pb.build_problem(p))
@@ -33,6 +37,7 @@ def _evolve(engine, params, t, dense):
         states = [engine.state(i) for i in range(len(params))]
     finally:
         engine.set_option("dense", 1)
+        engine.set_option("eig_impl", 1)
     engine.clear()
     return obs, st, states
 
@@ -129,3 +134,31 @@ def test_dense_full_grid_n14_matches_chebyshev_prefix(engine):
     engine.clear()
     assert st2["dense_problems"] == 0 and st2["mode"] == 1
     assert np.max(np.abs(obs[:, :, :K + 1] - ch)) < 1e-9
+
+
+def test_half_eigensolver_config2_matches_exact_and_dsyevd(engine, golden):
+    tr = golden("traces_n12.npz")
+    t = tr["t"]
+    p = sweep_point_params(11, 50000.0, "center_on", float(t[-1]), len(t))
+    hm, st, s_hm = _evolve(engine, [p], t, 2, eig_impl=2)
+    ev, _, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st["dense_problems"] == 1
+    for j, k in enumerate(OBS):
+        err = np.max(np.abs(hm[0, j] - tr[f"exact_{k}"]))
+        assert err < 1e-10, (k, err)
+    assert np.max(np.abs(hm - ev)) < 1e-11
+    assert np.max(np.abs(s_hm[0] - s_ev[0])) < 1e-11
+
+
+def test_half_eigensolver_n13_matches_dsyevd(engine):
+    t = np.linspace(0.0, 1.0, 2001)
+    p = sweep_point_params(12, 100e3, "center_on", 1.0, 2001)
+    hm, st, s_hm = _evolve(engine, [p], t, 2, eig_impl=1)
+    ev, _, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st["dense_problems"] == 1
+    np.testing.assert_allclose(hm[:, 6], 1.0, atol=1e-10)
+    # two eigensolvers agree to rounding: eigenvalues within ~1e-15 ||H||, so phases drift apart
+    # by ~1e-15 ||H|| t (3e-9 measured at t = 1 s); 1e-11 + 1e-8 t / (1 s)
+    tol = 1e-11 + 1e-8 * t
+    assert np.all(np.abs(hm - ev) <= tol), np.max(np.abs(hm - ev) - tol)
+    assert np.max(np.abs(s_hm[0] - s_ev[0])) < 1e-8
