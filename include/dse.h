@@ -169,11 +169,11 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "eig_streams"  dense engine: eigendecompositions of registers of >= 2^10 amplitudes
  *                         run this many at a time, one stream and rocBLAS handle each, 1..8
  *                         (default 2)
- *          "eig_impl"     dense engine eigensolver: 0 rocSOLVER dsyevd; 1 (default) the
- *                         half-matrix tridiagonalisation (dse_sytrd.hip) then rocSOLVER dstedc
- *                         and dormtr for registers of >= 2^13 amplitudes, dsyevd below; 2 the
- *                         half-matrix path from 2^10.  Costs one extra dim x dim matrix per
- *                         solver stream
+ *          "eig_impl"     dense engine eigensolver: 0 rocSOLVER dsyevd; 1 (default) for
+ *                         registers of >= 2^11 amplitudes a tridiagonalisation (the half-matrix
+ *                         one of dse_sytrd.hip from 2^13, rocSOLVER's below), rocSOLVER dstedc
+ *                         and a blocked back-transformation, dsyevd below 2^11; 2 the same from
+ *                         2^10.  Costs one extra dim x dim matrix per solver stream
  *          "matrix"       propagator-matrix mode for a lone register: 0 off, 1 by model
  *                         (default), 2 whenever eligible
  *          "symv_fused"   propagator-matrix mode: 1 sums each product's partials inside the

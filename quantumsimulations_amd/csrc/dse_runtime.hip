@@ -224,10 +224,9 @@ struct dse_ctx {
   // host thread, stream and rocBLAS handle each; option "eig_streams", default 2: measured 0.88 of
   // the one-by-one time per solve at 2^14, 0.81 at 2^13, profiles/r03/eig_concurrency_*.jsonl)
   int eig_streams = 2;
-  // dense engine eigensolver: 0 rocSOLVER dsyevd at every size; 1 the half-matrix tridiagonalisation
-  // (dse_sytrd.hip) + rocSOLVER dstedc / dormtr from kEigHalfMinDim amplitudes, dsyevd below
-  // (measured 3.03 vs 4.13 s at 2^14, 0.57 vs 0.68 s at 2^13, profiles/r03/sytrd_probe.jsonl);
-  // 2 the half-matrix path from 2^10 (tests)
+  // dense engine eigensolver: 0 rocSOLVER dsyevd at every size; 1 eig_sym_lower (dse_sytrd.hip: the
+  // half-matrix tridiagonalisation from 2^13, rocSOLVER dstedc, the blocked back-transformation)
+  // from kEigHalfMinDim amplitudes, dsyevd below; 2 eig_sym_lower from 2^10 (tests)
   int eig_impl = 1;
   std::vector<hipStream_t> eig_st;
   std::vector<rocblas_handle> eig_h;
@@ -1795,8 +1794,10 @@ struct DevArena {  // device allocations of one dense_run, freed on every exit p
 // (registers of one size) of a round is built, then all its eigendecompositions run on up to
 // eig_streams solver streams at once (largest first, across sizes), then the output GEMMs.
 // Blocking; writes obs_out.
-// the half-matrix eigensolver's crossover (eig_impl 1): 0.57 vs 0.68 s at 2^13, slower at 2^12
-constexpr size_t kEigHalfMinDim = 8192;
+// eig_impl 1 from 2^11 amplitudes: eig_sym_lower (rocSOLVER's tridiagonalisation below 2^13, the
+// half-matrix one above; dstedc; the 256-reflector back-transformation) against dsyevd measured
+// 0.47 vs 0.68 s at 2^13, 2.43 vs 4.12 s at 2^14 (profiles/r03/sytrd_probe.jsonl)
+constexpr size_t kEigHalfMinDim = 2048;
 
 struct DenseJob {
   int n = 0, cnt = 0, TB = 1;

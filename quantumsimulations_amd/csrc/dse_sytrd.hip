@@ -23,12 +23,13 @@
 // W' + alpha v from the W' and v entries it loads anyway (k_trd_wfix finalises the panel for the
 // update).  Then A(i+NB:n, i+NB:n) -= V W^T + W V^T (rocBLAS dsyr2k); the last columns by
 // rocsolver_dsytd2.  Per column: 4 launches, all reductions in fixed order (deterministic).
-// d, e, tau and the reflectors below the subdiagonal follow LAPACK's layout, so rocsolver_dstedc
-// (tridiagonal eigenvectors) and rocsolver_dormtr (V = Q Z) finish the decomposition.
+// d, e, tau and the reflectors below the subdiagonal follow LAPACK's layout: rocsolver_dstedc gives
+// the tridiagonal eigenvectors Z, ormtr_lower (blocks of 256 reflectors) V = Q Z.
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -47,7 +48,15 @@ struct TrdWs {
   double* dpart;    // nbk x 2 NB: partial u2', u3
   double* apart;    // nbk: partial W'(:, j).v
   double* alpha;    // NB
+  double* sspart;   // ceil(n / 256): k_trd_colref's partial sums of squares
+  double* scale;    // 1: the reflector's 1 / (alpha - beta) until k_trd_wfin applies it (1 when applied)
+  int* cnt;         // 1: k_trd_colref's workgroups done (zero between launches)
 };
+
+// v(r) of the current reflector: A(c+1, c) stands for 1, the rows below are scaled lazily
+__device__ __forceinline__ double refl_v(const double* col, int r, int c, double scale) {
+  return r == c + 1 ? 1.0 : scale * col[r];
+}
 
 // wave sum in fixed order, lane 0's value
 __device__ __forceinline__ double wave_sum0(double v) {
@@ -117,10 +126,74 @@ k_trd_colupd(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, i
   A[(size_t)c * lda + r] = s;
 }
 
+// 1 + 2 in one launch: the column update (j > 0) and the sums of squares of A(c+2:n, c) by block;
+// the last workgroup to finish (agent-scope counter) forms beta, tau and the scale of the reflector,
+// which k_trd_symv and k_trd_wfin apply as they read it (k_trd_wfin stores v).
+__global__ void __launch_bounds__(256)
+k_trd_colref(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int c, int j,
+             double* __restrict__ d, double* __restrict__ e, double* __restrict__ tau, int nbk_prev) {
+  __shared__ double s_al[kTrdNB];
+  __shared__ double red[4];
+  __shared__ int s_last;
+  if (j > 0) {
+    load_alpha(ws, tau, c, j, nbk_prev, s_al);
+    if (blockIdx.x == 0 && threadIdx.x == 0) ws.alpha[j - 1] = s_al[j - 1];
+  }
+  const int r = c + (int)(blockIdx.x * 256 + threadIdx.x);
+  double s = 0.0;
+  if (r < n) {
+    s = A[(size_t)c * lda + r];
+    if (j > 0) {
+      const double* W = ws.W;
+#pragma unroll 8
+      for (int p = 0; p < j; ++p) {
+        const double vr = A[(size_t)(i + p) * lda + r], vc = A[(size_t)(i + p) * lda + c];
+        const double wr = fma(s_al[p], vr, W[(size_t)p * ldw + (r - i)]);
+        const double wc = fma(s_al[p], vc, W[(size_t)p * ldw + (c - i)]);
+        s -= vr * wc + wr * vc;
+      }
+      A[(size_t)c * lda + r] = s;
+    }
+  }
+  const double ss = block_sum(r >= c + 2 && r < n ? s * s : 0.0, red);
+  if (threadIdx.x == 0) ws.sspart[blockIdx.x] = ss;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int last = __hip_atomic_fetch_add(ws.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last || threadIdx.x >= 64) return;
+  double xn2 = 0.0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 64) xn2 += __builtin_nontemporal_load(ws.sspart + b);
+  xn2 = wave_sum0(xn2);
+  if (threadIdx.x != 0) return;
+  const double* col = A + (size_t)c * lda;
+  const double alpha = __builtin_nontemporal_load(col + c + 1);
+  double t = 0.0, beta = alpha, scale = 1.0;
+  if (xn2 > 0.0) {
+    beta = -std::copysign(std::sqrt(alpha * alpha + xn2), alpha);
+    t = (beta - alpha) / beta;
+    scale = 1.0 / (alpha - beta);
+  }
+  d[c] = __builtin_nontemporal_load(col + c);
+  e[c] = beta;
+  tau[c] = t;
+  *ws.scale = scale;
+  *ws.cnt = 0;
+}
+
 // 2. reflector H = I - tau v v^T with H (alpha, x)^T = (beta, 0); alpha = A(c+1, c), x = A(c+2:n, c)
 __global__ void __launch_bounds__(1024)
 k_trd_larfg(double* __restrict__ A, int lda, int n, int c, double* __restrict__ d, double* __restrict__ e,
-            double* __restrict__ tau) {
+            double* __restrict__ tau, double* __restrict__ ws_scale) {
   __shared__ double red[16];
   __shared__ double s_scale;
   double* col = A + (size_t)c * lda;
@@ -144,6 +217,7 @@ k_trd_larfg(double* __restrict__ A, int lda, int n, int c, double* __restrict__ 
   __syncthreads();
   const double scale = s_scale;
   for (int r = c + 2 + (int)threadIdx.x; r < n; r += 1024) col[r] *= scale;
+  if (threadIdx.x == 0) *ws_scale = 1.0;
 }
 
 // 3. y = S v for the trailing block S = A(o:o+m, o:o+m) (lower triangle valid), v = A(o:o+m, c):
@@ -165,11 +239,12 @@ k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int 
   __shared__ double red[4][BS];
   __shared__ double tr[BS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const double* v = A + (size_t)c * lda + o;
+  const double* col = A + (size_t)c * lda;
   if (tid < BS) {
+    const double scale = *ws.scale;
     const int cj = J * BS + tid, ri = I * BS + tid;
-    vs[0][tid] = cj < m ? v[cj] : 0.0;
-    vs[1][tid] = ri < m ? v[ri] : 0.0;
+    vs[0][tid] = cj < m ? refl_v(col, o + cj, c, scale) : 0.0;
+    vs[1][tid] = ri < m ? refl_v(col, o + ri, c, scale) : 0.0;
   }
   __syncthreads();
   const int row = I * BS + lane;
@@ -239,7 +314,7 @@ k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int 
 // blockIdx.x; y from the symv partials, u2 = u2' + alpha u3 from the diagonal tiles' partials.
 // Leaves the block's W'(:, j).v in apart[B].  512 threads: 8 waves split the partials and the panel.
 __global__ void __launch_bounds__(512)
-k_trd_wfin(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int c, int j, int nbk,
+k_trd_wfin(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int c, int j, int nbk,
            const double* __restrict__ tau) {
   constexpr int BS = kTrdBS;
   __shared__ double su[2 * kTrdNB];
@@ -250,6 +325,7 @@ k_trd_wfin(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int 
     const int q = tid >> 3, sub = tid & 7;
     double s = 0.0;
     if (q < 2 * j)
+#pragma unroll 8
       for (int k = sub; k < nbk; k += 8) s += ws.dpart[(size_t)k * 2 * kTrdNB + q];
     s += __shfl_xor(s, 4, 64);
     s += __shfl_xor(s, 2, 64);
@@ -277,6 +353,7 @@ k_trd_wfin(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int 
       y += p3;
     }
     for (; k < nbk; k += 8) y += pp[(size_t)k * BS];
+#pragma unroll 4
     for (int p = w; p < j; p += 8) {
       const double vr = A[(size_t)(i + p) * lda + r];
       const double wr = fma(s_al[p], vr, ws.W[(size_t)p * ldw + (r - i)]);
@@ -293,7 +370,10 @@ k_trd_wfin(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int 
     double prod = 0.0;
     if (live) {
       ws.W[(size_t)j * ldw + (r - i)] = wv;
-      prod = wv * A[(size_t)c * lda + r];
+      double* col = A + (size_t)c * lda;
+      const double v = refl_v(col, r, c, *ws.scale);
+      col[r] = v;
+      prod = wv * v;
     }
     prod = wave_sum0(prod);
     if (tid == 0) ws.apart[B] = prod;
@@ -314,6 +394,34 @@ k_trd_wfix(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int 
   }
 }
 
+// ---- back-transformation V = Q Z, Q = H(0) H(1) ... H(n-2) (LAPACK dormtr, left, lower) ----
+// Blocks of kOrmKB reflectors from the last to the first, each applied as I - Vb T Vb^T in the
+// "UT" form T = S^{-1}, S = diag(1 / tau) + striu(Vb^T Vb): Wt = Vb^T Z_b (GEMM), Wt = S^{-1} Wt
+// (TRSM), Z_b -= Vb Wt (GEMM), where Z_b = the rows i+1 .. n-1 the block acts on.  A block of 256
+// reflectors reads Z_b three times (rocSOLVER dormtr's blocks of 32: ~24 passes over the same
+// rows; measured 769 ms at 2^14, 11 TF/s).  A reflector with tau = 0 (H = I: its column was zero
+// already) gets a zero column in Vb and 1 on S's diagonal, so it changes nothing.
+constexpr int kOrmKB = 256;
+constexpr int kHalfTrdMinDim = 8192;
+
+// Vb (m_b x k, column-major): unit lower trapezoid of the reflectors i .. i+k-1 (rows i+1 .. n-1)
+__global__ void __launch_bounds__(256)
+k_orm_vb(const double* __restrict__ A, int lda, const double* __restrict__ tau, int i, int k, int m_b,
+         double* __restrict__ Vb) {
+  const int r = (int)(blockIdx.x * 256 + threadIdx.x), q = (int)blockIdx.y;
+  if (r >= m_b) return;
+  double v = 0.0;
+  if (tau[i + q] != 0.0) v = r > q ? A[(size_t)(i + q) * lda + (i + 1 + r)] : r == q ? 1.0 : 0.0;
+  Vb[(size_t)q * m_b + r] = v;
+}
+
+__global__ void k_orm_sdiag(double* __restrict__ S, int k, const double* __restrict__ tau, int i) {
+  const int q = (int)threadIdx.x + (int)blockIdx.x * 256;
+  if (q >= k) return;
+  const double t = tau[i + q];
+  S[(size_t)q * k + q] = t != 0.0 ? 1.0 / t : 1.0;
+}
+
 TrdWs carve(double* work, int n) {
   const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS;
   TrdWs ws;
@@ -322,6 +430,9 @@ TrdWs carve(double* work, int n) {
   ws.dpart = ws.partial + nbk * nbk * kTrdBS;
   ws.apart = ws.dpart + nbk * 2 * kTrdNB;
   ws.alpha = ws.apart + nbk;
+  ws.sspart = ws.alpha + kTrdNB;
+  ws.scale = ws.sspart + (n + 255) / 256;
+  ws.cnt = reinterpret_cast<int*>(ws.scale + 1);
   return ws;
 }
 
@@ -329,22 +440,61 @@ TrdWs carve(double* work, int n) {
 
 size_t sytrd_workspace(int n) {
   const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS;
-  return ((size_t)n * kTrdNB + nbk * nbk * kTrdBS + nbk * 2 * kTrdNB + nbk + kTrdNB) * sizeof(double);
+  const size_t trd =
+      (size_t)n * kTrdNB + nbk * nbk * kTrdBS + nbk * 2 * kTrdNB + nbk + kTrdNB + ((size_t)n + 255) / 256 + 2;
+  const size_t orm = 2 * (size_t)n * kOrmKB + (size_t)kOrmKB * kOrmKB;  // Vb, Wt, S
+  return std::max(trd, orm) * sizeof(double);
+}
+
+int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, const double* tau, double* Z,
+                int ldz, double* work) {
+  const int nref = n - 1;
+  if (nref <= 0) return 0;
+  double* Vb = work;
+  double* Wt = Vb + (size_t)n * kOrmKB;
+  double* S = Wt + (size_t)n * kOrmKB;
+  const double one = 1.0, zero = 0.0, minus_one = -1.0;
+  const int nblk = (nref + kOrmKB - 1) / kOrmKB;
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int i = b * kOrmKB, k = std::min(kOrmKB, nref - i), m_b = n - i - 1;
+    hipLaunchKernelGGL(k_orm_vb, dim3((m_b + 255) / 256, k), dim3(256), 0, st, A, lda, tau, i, k, m_b, Vb);
+    if (hipGetLastError() != hipSuccess) return -6;
+    if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, k, k, m_b, &one, Vb, m_b, Vb, m_b, &zero,
+                      S, k) != rocblas_status_success)
+      return -7;
+    hipLaunchKernelGGL(k_orm_sdiag, dim3((k + 255) / 256), dim3(256), 0, st, S, k, tau, i);
+    if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, k, n, m_b, &one, Vb, m_b, Z + i + 1, ldz,
+                      &zero, Wt, k) != rocblas_status_success)
+      return -7;
+    if (rocblas_dtrsm(h, rocblas_side_left, rocblas_fill_upper, rocblas_operation_none, rocblas_diagonal_non_unit, k,
+                      n, &one, S, k, Wt, k) != rocblas_status_success)
+      return -8;
+    if (rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, m_b, n, k, &minus_one, Vb, m_b, Wt, k, &one,
+                      Z + i + 1, ldz) != rocblas_status_success)
+      return -7;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -6;
 }
 
 int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* d, double* e, double* tau,
-                double* work) {
+                double* work, int fused) {
   const TrdWs ws = carve(work, n);
   const int ldw = n;
+  if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
   int i = 0;
   for (; n - i > kTrdRem + kTrdNB; i += kTrdNB) {
     int nbk_prev = 0;
     for (int j = 0; j < kTrdNB; ++j) {
       const int c = i + j;
-      if (j > 0)
-        hipLaunchKernelGGL(k_trd_colupd, dim3((n - c + 255) / 256), dim3(256), 0, st, A, lda, ws, ldw, n, i, c, j,
-                           tau, nbk_prev);
-      hipLaunchKernelGGL(k_trd_larfg, dim3(1), dim3(1024), 0, st, A, lda, n, c, d, e, tau);
+      if (fused) {
+        hipLaunchKernelGGL(k_trd_colref, dim3((n - c + 255) / 256), dim3(256), 0, st, A, lda, ws, ldw, n, i, c, j, d,
+                           e, tau, nbk_prev);
+      } else {
+        if (j > 0)
+          hipLaunchKernelGGL(k_trd_colupd, dim3((n - c + 255) / 256), dim3(256), 0, st, A, lda, ws, ldw, n, i, c, j,
+                             tau, nbk_prev);
+        hipLaunchKernelGGL(k_trd_larfg, dim3(1), dim3(1024), 0, st, A, lda, n, c, d, e, tau, ws.scale);
+      }
       const int o = c + 1, m = n - o;
       const int nbk = (m + kTrdBS - 1) / kTrdBS;
       hipLaunchKernelGGL(k_trd_symv, dim3(nbk * (nbk + 1) / 2), dim3(256), 0, st, A, lda, ws, ldw, i, j, o, m, c,
@@ -371,13 +521,17 @@ int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, dou
 
 int eig_sym_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
                   double* e, double* tau, double* work, int* info) {
-  int rc = sytrd_lower(h, st, n, A, lda, lam, e, tau, work);
-  if (rc) return rc;
+  // below 2^13 rocSOLVER's tridiagonalisation is the faster one (per-column launch latency
+  // outweighs the halved reads: 101 vs 112 ms at 2^12, profiles/r03/sytrd_probe.jsonl); the
+  // fused column kernel pays its cross-XCD release only where the columns are long
+  if (n >= kHalfTrdMinDim) {
+    const int rc = sytrd_lower(h, st, n, A, lda, lam, e, tau, work, n >= 16384 ? 1 : 0);
+    if (rc) return rc;
+  } else if (rocsolver_dsytrd(h, rocblas_fill_lower, n, A, lda, lam, e, tau) != rocblas_status_success) {
+    return -3;
+  }
   if (rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, ldv, info) != rocblas_status_success) return -4;
-  if (rocsolver_dormtr(h, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none, n, n, A, lda, tau, V, ldv) !=
-      rocblas_status_success)
-    return -5;
-  return 0;
+  return ormtr_lower(h, st, n, A, lda, tau, V, ldv, work);
 }
 
 }  // namespace dse

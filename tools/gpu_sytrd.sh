@@ -1,18 +1,16 @@
 #!/bin/bash
-# Half-matrix tridiagonalisation (dse_sytrd.hip) vs rocSOLVER: accuracy at 2^11..2^13, timing up to 2^14,
-# then the kernel split of one 2^13 run.
+# Half-matrix tridiagonalisation (dse_sytrd.hip) vs rocSOLVER: accuracy at 2^11..2^14 with timings,
+# then the phases and kernel split of sytrd_lower at $PROF_DIM (default 16384).
 set -o pipefail
 OUT=gpurun_out/r03/sytrd${TAG:-3}
 trap "rm -f $OUT/trace/s_kernel_trace.csv" EXIT
 mkdir -p $OUT
 export TMPDIR=/tmp
-for n in 2048 4096 8192; do
-  timeout -k 10 120 tools/bin/probe_sytrd $n check >> $OUT/probe.jsonl 2>> $OUT/err.txt || { echo "fail $n $?"; cat $OUT/err.txt; exit 1; }
+for n in ${DIMS:-2048 4096 8192 16384}; do
+  timeout -k 10 200 tools/bin/probe_sytrd $n check >> $OUT/probe.jsonl 2>> $OUT/err.txt || { echo "fail $n $?"; cat $OUT/err.txt; exit 1; }
 done
 cat $OUT/probe.jsonl
-timeout -k 10 200 tools/bin/probe_sytrd 16384 check >> $OUT/probe.jsonl 2>> $OUT/err.txt || { echo "fail 16384"; exit 1; }
-tail -9 $OUT/probe.jsonl
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/trace -o s --output-format csv -- tools/bin/probe_sytrd 8192 > $OUT/prof.jsonl 2>> $OUT/err.txt && \
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/trace -o s --output-format csv -- tools/bin/probe_sytrd ${PROF_DIM:-16384} split > $OUT/prof.jsonl 2>> $OUT/err.txt && cat $OUT/prof.jsonl && \
 python3 -c "
 import csv
 rows=list(csv.DictReader(open('$OUT/trace/s_kernel_stats.csv')))

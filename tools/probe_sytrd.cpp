@@ -1,7 +1,7 @@
 // Probe (round 3): the half-matrix tridiagonalisation (dse_sytrd.hip) against rocSOLVER.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iquantumsimulations_amd/csrc tools/probe_sytrd.cpp \
 //         quantumsimulations_amd/csrc/dse_sytrd.hip -lrocsolver -lrocblas -o /tmp/probe_sytrd
-//   probe_sytrd <dim> [check]
+//   probe_sytrd <dim> [check | split]
 // Matrix as tools/probe_eig.cpp (spectrum and sparsity of the N = 14 rotated H').  Prints one JSON
 // line per timing and, with check, max |lam - lam_dsyevd| / max |lam|, max |A V - V diag(lam)| /
 // max |lam| and max |V^T V - I|.
@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "dse_dense.h"
@@ -55,7 +56,7 @@ static double now_ms() {
 
 int main(int argc, char** argv) {
   const int n = argc > 1 ? std::atoi(argv[1]) : 2048;
-  const bool check = argc > 2;
+  const bool check = argc > 2 && std::string(argv[2]) == "check";
   int nbits = 0;
   while ((1 << nbits) < n) ++nbits;
   const size_t nn = (size_t)n * n;
@@ -97,9 +98,44 @@ int main(int argc, char** argv) {
   CK(hipMemsetAsync(lam, 0, n * 8, st));
   dse::eig_sym_lower(h, st, n, A, n, lam, V, n, e, tau, work, info);
   CK(hipStreamSynchronize(st));
+  if (argc > 2 && std::string(argv[2]) == "split") {
+    // the phases of eig_sym_lower, and sytrd_lower alone three times (for kernel traces)
+    for (int rep = 0; rep < 3; ++rep) timed("sytrd_lower", [&] { return dse::sytrd_lower(h, st, n, A, n, lam, e, tau, work); });
+    reset();
+    dse::sytrd_lower(h, st, n, A, n, lam, e, tau, work);
+    CK(hipStreamSynchronize(st));
+    double t0 = now_ms();
+    rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, n, info);
+    CK(hipStreamSynchronize(st));
+    double t1 = now_ms();
+    // Z kept in V0 for the second back-transformation
+    const double ms_stedc = t1 - t0;
+    double* V0 = A0;  // A0 no longer needed
+    CK(hipMemcpyAsync(V0, V, nn * 8, hipMemcpyDeviceToDevice, st));
+    CK(hipStreamSynchronize(st));
+    t1 = now_ms();
+    rocsolver_dormtr(h, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none, n, n, A, n, tau, V, n);
+    CK(hipStreamSynchronize(st));
+    double t2 = now_ms();
+    const int rc = dse::ormtr_lower(h, st, n, A, n, tau, V0, n, work);
+    CK(hipStreamSynchronize(st));
+    double t3 = now_ms();
+    // max |V_dormtr - V_ormtr_lower|
+    const double mone = -1.0;
+    rocblas_daxpy(h, (rocblas_int)std::min(nn, (size_t)0x7fffffff), &mone, V, 1, V0, 1);
+    rocblas_int ia = 0;
+    rocblas_idamax(h, (rocblas_int)std::min(nn, (size_t)0x7fffffff), V0, 1, &ia);
+    double dv = 0.0;
+    CK(hipMemcpy(&dv, V0 + (ia - 1), 8, hipMemcpyDeviceToHost));
+    std::printf("{\"dim\": %d, \"op\": \"dstedc\", \"ms\": %.1f}\n{\"dim\": %d, \"op\": \"dormtr\", \"ms\": %.1f}\n"
+                "{\"dim\": %d, \"op\": \"ormtr_lower\", \"ms\": %.1f, \"rc\": %d, \"max_diff_vs_dormtr\": %.3e}\n",
+                n, ms_stedc, n, t2 - t1, n, t3 - t2, rc, std::fabs(dv));
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     timed("rocsolver_dsytrd", [&] { return (int)rocsolver_dsytrd(h, rocblas_fill_lower, n, A, n, lam, e, tau); });
     timed("sytrd_lower", [&] { return dse::sytrd_lower(h, st, n, A, n, lam, e, tau, work); });
+    timed("sytrd_lower_unfused", [&] { return dse::sytrd_lower(h, st, n, A, n, lam, e, tau, work, 0); });
     timed("rocsolver_dsyevd", [&] {
       return (int)rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_lower, n, A, n, lref, e, info);
     });
