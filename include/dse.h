@@ -155,9 +155,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "obs_overlap"  persistent mode: 1 runs each interval group's observables on a second
  *                         stream per lane (lowest priority) while the next group's launches run,
  *                         with two sets of intermediate-output accumulators; 0 (default) in line
- *          "mixed_launch" persistent mode: 1 puts the 1- and 2-tile problems of one tile size in
- *                         one interval launch (stiffest pairs, 1-tile problems, remaining pairs)
- *                         when all 2-tile workgroups fit at once; 0 (default) one stream each
+ *          "mixed_launch" persistent mode: 1 (default) puts the 1- and 2-tile problems of one tile
+ *                         size in one interval launch (stiffest pairs, 1-tile problems, remaining
+ *                         pairs) when all 2-tile workgroups fit at once; 0 one stream each
  *          "handoff_fences"  persistent mode, 2-tile registers: 0 (default) the sc1 hand-off
  *                         (write-through payload, per-wave vmcnt(0) + barrier, sc1 flag and
  *                         poll); 1 adds an agent-scope release before every flag store and an

@@ -149,7 +149,7 @@ struct dse_ctx {
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
-  int mixed_launch = 0;             // persistent: 1- and 2-tile problems of one tile size in one launch
+  int mixed_launch = 1;             // persistent: 1- and 2-tile problems of one tile size in one launch
   int obs_overlap = 0;              // persistent: observables off the interval launches' stream
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)

@@ -135,10 +135,10 @@ def test_reference_grid_intervals_match_fine_stepping_n14(engine):
 
 
 def test_mixed_launch_is_bitwise_identical(engine):
-    """Option mixed_launch: the 1- and 2-tile problems of the config-3 points in one interval launch
-    (stiffest pairs, then the 1-tile problems, then the remaining pairs) instead of one stream
-    each.  Only the dispatch order changes, so every problem's results are bitwise those of the
-    default two-stream schedule, and the run stays on the persistent kernel."""
+    """Option mixed_launch (default 1): the 1- and 2-tile problems of the config-3 points in one
+    interval launch (stiffest pairs, then the 1-tile problems, then the remaining pairs) instead of
+    one stream each (0).  Only the dispatch order changes, so every problem's results are bitwise
+    those of the two-stream schedule, and the run stays on the persistent kernel."""
     t = np.linspace(0.0, 2e-4, 21)
     res = {}
     for mixed in (0, 1, 1):
@@ -150,7 +150,7 @@ def test_mixed_launch_is_bitwise_identical(engine):
                     engine.add(pb.build_problem(_params(variant, delta, t)))
             obs, st = engine.evolve(t)
         finally:
-            engine.set_option("mixed_launch", 0)
+            engine.set_option("mixed_launch", 1)
             engine.clear()
         assert st["mode"] == 1
         if mixed in res:
