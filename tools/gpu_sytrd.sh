@@ -3,7 +3,7 @@
 # then the phases and kernel split of sytrd_lower at $PROF_DIM (default 16384).
 set -o pipefail
 OUT=gpurun_out/r03/sytrd${TAG:-3}
-trap "rm -f $OUT/trace/s_kernel_trace.csv" EXIT
+trap "rm -f $OUT/trace/s_kernel_trace.csv" EXIT  # too large to bring back; summarised on the box
 mkdir -p $OUT
 export TMPDIR=/tmp
 for n in ${DIMS:-2048 4096 8192 16384}; do
@@ -17,3 +17,4 @@ rows=list(csv.DictReader(open('$OUT/trace/s_kernel_stats.csv')))
 rows.sort(key=lambda r:-float(r['TotalDurationNs']))
 for r in rows[:25]: print(r['Calls'].rjust(6), ('%.1f ms' % (float(r['TotalDurationNs'])/1e6)).rjust(10), ('%.1f us' % (float(r['AverageNs'])/1e3)).rjust(10), r['Name'][:110])
 "
+python3 tools/symv_curve.py $OUT/trace/s_kernel_trace.csv ${PROF_DIM:-16384}
