@@ -65,11 +65,10 @@ namespace dse {
 
 // ---- the half-matrix tridiagonalisation (dse_sytrd.hip): LAPACK dsytrd's lower layout (d, e, tau,
 // reflectors below the subdiagonal of A), the trailing-matrix products over the lower-triangle
-// tiles only.  work: sytrd_workspace(n) bytes.  fused: the column update and the reflector in one
-// launch (k_trd_colref); 0: two (probe A/B).  0 on success.
+// tiles only.  work: sytrd_workspace(n) bytes.  0 on success.
 size_t sytrd_workspace(int n);
 int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* d, double* e, double* tau,
-                double* work, int fused = 1);
+                double* work);
 // Z = Q Z for the Q of sytrd_lower's reflectors in A (rocsolver_dormtr's left / lower / no-transpose
 // case), blocks of 256 reflectors; work: sytrd_workspace(n) bytes
 int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, const double* tau, double* Z,

@@ -165,7 +165,6 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   const int tid = threadIdx.x;
   const bool pair = (P.n == L + 1);
   const bool xgen = pair && P.n_pairs_hi > 0;  // pairs cross the tile boundary: u pre-pass
-  const bool xraw = pair && !xgen;             // only the top-bit drive crosses: raw w exchange
   const int K = P.degree;
   const double s1 = P.s1;
   const uint32_t b_me = h & 1u, b_pa = b_me ^ 1u;  // top-bit values of this / the partner tile

@@ -30,6 +30,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <deque>
 #include <vector>
 
 #include <unistd.h>
@@ -1968,12 +1969,23 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         half_min = SIZE_MAX;
       }
     }
+    // the workers take tasks largest first; a job whose last register is solved goes to the output
+    // queue, and this thread runs its output GEMMs (dense_stream) while the other jobs' solves go on
+    // (a round's 2^14 registers' outputs under its 2^13 solve)
     std::atomic<size_t> next{0};
+    std::atomic<bool> abort_all{false};
     std::vector<rocblas_status> wst(K, rocblas_status_success);
     std::vector<int> wrc(K, 0);
     std::vector<hipError_t> werr(K, hipSuccess);
+    std::mutex qm;
+    std::condition_variable qcv;
+    std::deque<DenseJob*> ready;
+    std::map<DenseJob*, int> pending;
+    for (const Task& T : tasks) pending[T.j] += 1;
+    int workers_left = K;
+    auto e1 = e0;
     auto worker = [&](int w) {
-      for (size_t ti = next++; ti < tasks.size() && wst[w] == rocblas_status_success && wrc[w] == 0; ti = next++) {
+      for (size_t ti = next++; ti < tasks.size() && !abort_all; ti = next++) {
         const Task& T = tasks[ti];
         DenseJob& J = *T.j;
         const rocblas_int dim = (rocblas_int)J.dim;
@@ -1982,9 +1994,9 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           double* Vi = J.V + J.dim * J.dim * i;
           werr[w] = hipMemcpyAsync(scr[w].A, Vi, J.dim * J.dim * sizeof(double), hipMemcpyDeviceToDevice,
                                    ctx->eig_st[w]);
-          if (werr[w] != hipSuccess) break;
-          wrc[w] = eig_sym_lower(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
-                                 J.E + J.dim * i, scr[w].tau, scr[w].work, J.info + i);
+          if (werr[w] == hipSuccess)
+            wrc[w] = eig_sym_lower(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
+                                   J.E + J.dim * i, scr[w].tau, scr[w].work, J.info + i);
         } else if (T.i >= 0) {
           const size_t i = (size_t)T.i;
           wst[w] = rocsolver_dsyevd(ctx->eig_h[w], rocblas_evect_original, rocblas_fill_upper, dim,
@@ -1994,29 +2006,23 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
                                                     J.V, dim, (rocblas_stride)(J.dim * J.dim), J.lam,
                                                     (rocblas_stride)J.dim, J.E, (rocblas_stride)J.dim, J.info, J.cnt);
         }
+        const hipError_t se = hipStreamSynchronize(ctx->eig_st[w]);
+        if (werr[w] == hipSuccess) werr[w] = se;
+        if (werr[w] != hipSuccess || wst[w] != rocblas_status_success || wrc[w] != 0) {
+          abort_all = true;
+          break;
+        }
+        std::lock_guard<std::mutex> lk(qm);
+        if (--pending[&J] == 0) {
+          ready.push_back(&J);
+          qcv.notify_one();
+        }
       }
-      const hipError_t se = hipStreamSynchronize(ctx->eig_st[w]);
-      if (werr[w] == hipSuccess) werr[w] = se;
+      std::lock_guard<std::mutex> lk(qm);
+      if (--workers_left == 0) e1 = std::chrono::steady_clock::now();
+      qcv.notify_one();
     };
-    if (K == 1) {
-      worker(0);
-    } else {
-      std::vector<std::thread> th;
-      for (int w = 0; w < K; ++w) th.emplace_back(worker, w);
-      for (auto& x : th) x.join();
-    }
-    for (int w = 0; w < K; ++w) {
-      if (werr[w] != hipSuccess)
-        return fail(ctx, DSE_ERR_HIP, std::string("eigensolver stream: ") + hipGetErrorString(werr[w]));
-      if (wst[w] != rocblas_status_success)
-        return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)wst[w]) + ")");
-      if (wrc[w] != 0)
-        return fail(ctx, DSE_ERR_HIP, "half-matrix eigensolver failed (step " + std::to_string(-wrc[w]) + ")");
-    }
-    eig_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e0).count();
-    // ---- outputs of every job of the round ----
-    for (auto& Jp : jobs) {
-      DenseJob& J = *Jp;
+    auto outputs = [&](DenseJob& J) -> int {
       const int cnt = J.cnt, TB = J.TB;
       const size_t dim = J.dim, pstride = J.pstride;
       std::vector<rocblas_int> hinfo(cnt);
@@ -2024,7 +2030,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       HIPC(hipStreamSynchronize(st));
       for (int i = 0; i < cnt; ++i)
         if (hinfo[i] != 0)
-          return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: dsyevd did not converge (info " +
+          return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: eigensolver did not converge (info " +
                                                     std::to_string(hinfo[i]) + ")");
       const double one = 1.0, zero = 0.0;
       for (int tb0 = 0; tb0 < n_t; tb0 += TB) {
@@ -2048,7 +2054,40 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           finish_obs(ctx->probs[pi], h.data() + ((size_t)i * n_t + ti) * 8,
                      obs_out + (size_t)pi * DSE_N_OBS * n_t + ti, (size_t)n_t);
       }
+      return DSE_OK;
+    };
+    std::vector<std::thread> th;
+    for (int w = 0; w < K; ++w) th.emplace_back(worker, w);
+    int orc = DSE_OK;
+    size_t done = 0;
+    while (done < jobs.size()) {
+      DenseJob* J = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(qm);
+        qcv.wait(lk, [&] { return !ready.empty() || workers_left == 0; });
+        if (ready.empty()) break;  // the workers stopped early: an error below
+        J = ready.front();
+        ready.pop_front();
+      }
+      orc = outputs(*J);
+      if (orc != DSE_OK) {
+        abort_all = true;
+        break;
+      }
+      ++done;
     }
+    for (auto& x : th) x.join();
+    if (orc != DSE_OK) return orc;
+    for (int w = 0; w < K; ++w) {
+      if (werr[w] != hipSuccess)
+        return fail(ctx, DSE_ERR_HIP, std::string("eigensolver stream: ") + hipGetErrorString(werr[w]));
+      if (wst[w] != rocblas_status_success)
+        return fail(ctx, DSE_ERR_HIP, "rocsolver dsyevd failed (status " + std::to_string((int)wst[w]) + ")");
+      if (wrc[w] != 0)
+        return fail(ctx, DSE_ERR_HIP, "half-matrix eigensolver failed (step " + std::to_string(-wrc[w]) + ")");
+    }
+    if (done < jobs.size()) return fail(ctx, DSE_ERR_HIP, "dense engine: eigensolver workers stopped early");
+    eig_ms += std::chrono::duration<double, std::milli>(e1 - e0).count();
   }
   if (ms_all) *ms_all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
   if (ms_eig) *ms_eig = eig_ms;

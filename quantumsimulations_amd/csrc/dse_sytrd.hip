@@ -1,30 +1,34 @@
 // dse_sytrd.hip -- symmetric eigendecomposition for the dense engine (dse_dense.h, option
 // "eig_impl" = 1): a blocked Householder tridiagonalisation of the lower triangle written for
-// gfx950, then rocSOLVER's tridiagonal divide and conquer (dstedc) and back-transformation
-// (dormtr).
+// gfx950, rocSOLVER's tridiagonal divide and conquer (dstedc) and a blocked back-transformation.
 //
 // Why: rocSOLVER dsyevd spends ~73% of a 2^14 solve in its tridiagonalisation (dsytrd 2.94 of
 // 4.04 s, profiles/r03/eig_concurrency_16384.jsonl), most of it in one matrix-vector product per
 // column against the trailing matrix, which it reads whole (latrd_lower_computeW_gemvt_kernel:
-// 38.5 us per column on average at 2^13, the trailing block's full bytes at ~4.7 TB/s).  The
+// 152 us per column on average at 2^14, the trailing block's full bytes at ~4.7 TB/s).  The
 // product is symmetric, so reading only the tiles on and below the diagonal and using each twice
 // halves those bytes.
 //
 // Algorithm (LAPACK dsytrd / dlatrd, lower): panels of NB columns; for column c of a panel starting
 // at column i (local j = c - i; W the panel's n x NB block, row r of W at r - i; v_p = A(:, i+p)):
-//   1. A(c:n, c) -= A(c:n, i:c) W(c, 0:j)^T + W(c:n, 0:j) A(c, i:c)^T          (k_trd_colupd)
-//   2. reflector of A(c+1:n, c): beta, tau, v (v_0 = 1 stored in A(c+1, c))     (k_trd_larfg)
-//   3. y = A(c+1:n, c+1:n) v over the lower-triangle tiles, partials per block;
-//      u2 = W(c+1:n, 0:j)^T v, u3 = A(c+1:n, i:c)^T v by the diagonal tiles     (k_trd_symv)
+//   1. A(c:n, c) -= A(c:n, i:c) W(c, 0:j)^T + W(c:n, 0:j) A(c, i:c)^T
+//   2. reflector of A(c+1:n, c): beta, tau, v (v_0 = 1 at A(c+1, c)); u2' = W'(c+1:n, 0:j)^T v,
+//      u3 = A(c+1:n, i:c)^T v                                                     (k_trd_colref)
+//   3. y = A(c+1:n, c+1:n) v over the lower-triangle tiles, partials per block  (k_trd_symv)
 //   4. W(c+1:n, j) = tau (y - A(c+1:n, i:c) u2 - W(c+1:n, 0:j) u3)              (k_trd_wfin)
 //   5. W(:, j) += alpha_j v, alpha_j = -tau/2 W(:, j).v
-// Step 5 is never a pass of its own: k_trd_wfin leaves W' = W - alpha v and per-block partial dots
-// of W'.v, the next column's k_trd_colupd sums them into alpha_j, and every reader of W forms
-// W' + alpha v from the W' and v entries it loads anyway (k_trd_wfix finalises the panel for the
-// update).  Then A(i+NB:n, i+NB:n) -= V W^T + W V^T (rocBLAS dsyr2k); the last columns by
-// rocsolver_dsytd2.  Per column: 4 launches, all reductions in fixed order (deterministic).
-// d, e, tau and the reflectors below the subdiagonal follow LAPACK's layout: rocsolver_dstedc gives
-// the tridiagonal eigenvectors Z, ormtr_lower (blocks of 256 reflectors) V = Q Z.
+// k_trd_colref's workgroups each update 256 rows of the column and leave their rows' share of
+// ||x||^2 and of the dot products of x with the panel's W' and V columns; the last workgroup to
+// finish (agent-scope counter) forms beta, tau, the reflector's scale and u2', u3 (v = scale x
+// below its leading 1, so the dots are the scaled sums plus the leading row).  The scale is applied
+// lazily: k_trd_symv scales v as it loads it, k_trd_wfin stores it.  Step 5 is never a pass of its
+// own: k_trd_wfin leaves W' = W - alpha v and per-block partial dots of W'.v, the next column's
+// k_trd_colref sums them into alpha_j, and every reader of W forms W' + alpha v from the W' and v
+// entries it loads anyway (k_trd_wfix finalises the panel for the update).  Then A(i+NB:n,
+// i+NB:n) -= V W^T + W V^T (rocBLAS dsyr2k); the last columns by rocsolver_dsytd2.  Three launches
+// per column, every reduction in fixed order (deterministic).  d, e, tau and the reflectors below
+// the subdiagonal follow LAPACK's layout: rocsolver_dstedc gives the tridiagonal eigenvectors Z,
+// ormtr_lower (blocks of 256 reflectors) V = Q Z.
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
@@ -41,11 +45,13 @@ namespace {
 constexpr int kTrdNB = 32;   // panel width
 constexpr int kTrdBS = 64;   // symv tile, rows per k_trd_wfin workgroup
 constexpr int kTrdRem = 64;  // columns left to rocsolver_dsytd2
+constexpr int kTrdRows = 256;  // rows per k_trd_colref workgroup
 
 struct TrdWs {
   double* W;        // n x NB, ldw = n
   double* partial;  // nbk x nbk x BS: symv partials
-  double* dpart;    // nbk x 2 NB: partial u2', u3
+  double* upart;    // ceil(n / 256) x 2 NB: k_trd_colref's partial x.W'(:, p) (slots < NB), x.v_p (>= NB)
+  double* u;        // 2 NB: u2' (slots < NB), u3 (slots >= NB) of the current column
   double* apart;    // nbk: partial W'(:, j).v
   double* alpha;    // NB
   double* sspart;   // ceil(n / 256): k_trd_colref's partial sums of squares
@@ -106,60 +112,70 @@ __device__ __forceinline__ void load_alpha(const TrdWs& ws, const double* tau, i
   __syncthreads();
 }
 
-// 1. column update, rows r in [c, n); j > 0.  Also alpha_{j-1} (workgroup 0 stores it).
-__global__ void __launch_bounds__(256)
-k_trd_colupd(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int c, int j, const double* tau,
-             int nbk_prev) {
-  __shared__ double s_al[kTrdNB];
-  load_alpha(ws, tau, c, j, nbk_prev, s_al);
-  if (blockIdx.x == 0 && threadIdx.x == 0) ws.alpha[j - 1] = s_al[j - 1];
-  const int r = c + (int)(blockIdx.x * 256 + threadIdx.x);
-  if (r >= n) return;
-  const double* W = ws.W;
-  double s = A[(size_t)c * lda + r];
-  for (int p = 0; p < j; ++p) {
-    const double vr = A[(size_t)(i + p) * lda + r], vc = A[(size_t)(i + p) * lda + c];
-    const double wr = fma(s_al[p], vr, W[(size_t)p * ldw + (r - i)]);
-    const double wc = fma(s_al[p], vc, W[(size_t)p * ldw + (c - i)]);
-    s -= vr * wc + wr * vc;
-  }
-  A[(size_t)c * lda + r] = s;
-}
-
-// 1 + 2 in one launch: the column update (j > 0) and the sums of squares of A(c+2:n, c) by block;
-// the last workgroup to finish (agent-scope counter) forms beta, tau and the scale of the reflector,
-// which k_trd_symv and k_trd_wfin apply as they read it (k_trd_wfin stores v).
-__global__ void __launch_bounds__(256)
+// 1 + 2: the column update (j > 0), and per workgroup of 256 rows the sum of squares of x =
+// A(c+2:n, c) and the dots x.W'(:, p), x.v_p; the last workgroup forms the reflector and u2', u3.
+__global__ void __launch_bounds__(kTrdRows)
 k_trd_colref(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int c, int j,
              double* __restrict__ d, double* __restrict__ e, double* __restrict__ tau, int nbk_prev) {
   __shared__ double s_al[kTrdNB];
+  __shared__ double s_vc[kTrdNB], s_wc[kTrdNB];  // row c of the panel: A(c, i+p), W(c-i, p) final
   __shared__ double red[4];
+  __shared__ double ured[4][2 * kTrdNB];
   __shared__ int s_last;
+  const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = c + (int)blockIdx.x * kTrdRows + tid;
+  const double* W = ws.W;
+  double s = r < n ? A[(size_t)c * lda + r] : 0.0;
   if (j > 0) {
+    // alpha (wave 0 sums, threads 64.. load), row c of V and W' (threads 128.., 192..)
+    const int tq = tid - 128, tw = tid - 192;
+    if (tq >= 0 && tq < j) s_vc[tq] = A[(size_t)(i + tq) * lda + c];
+    if (tw >= 0 && tw < j) s_wc[tw] = W[(size_t)tw * ldw + (c - i)];
+    // all of the row's panel loads at once, in flight under the alpha prologue (p >= j: column i
+    // again, dropped by the selects)
+    double vr[kTrdNB], wr[kTrdNB];
+#pragma unroll
+    for (int p = 0; p < kTrdNB; ++p) {
+      const int pp = p < j ? p : 0;
+      vr[p] = r < n ? A[(size_t)(i + pp) * lda + r] : 0.0;
+      wr[p] = r < n ? W[(size_t)pp * ldw + (r - i)] : 0.0;
+    }
     load_alpha(ws, tau, c, j, nbk_prev, s_al);
-    if (blockIdx.x == 0 && threadIdx.x == 0) ws.alpha[j - 1] = s_al[j - 1];
-  }
-  const int r = c + (int)(blockIdx.x * 256 + threadIdx.x);
-  double s = 0.0;
-  if (r < n) {
-    s = A[(size_t)c * lda + r];
-    if (j > 0) {
-      const double* W = ws.W;
-#pragma unroll 8
-      for (int p = 0; p < j; ++p) {
-        const double vr = A[(size_t)(i + p) * lda + r], vc = A[(size_t)(i + p) * lda + c];
-        const double wr = fma(s_al[p], vr, W[(size_t)p * ldw + (r - i)]);
-        const double wc = fma(s_al[p], vc, W[(size_t)p * ldw + (c - i)]);
-        s -= vr * wc + wr * vc;
+    if (tid < j) s_wc[tid] = fma(s_al[tid], s_vc[tid], s_wc[tid]);
+    if (blockIdx.x == 0 && tid == 0) ws.alpha[j - 1] = s_al[j - 1];
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < kTrdNB; ++p) {
+      const int pp = p < j ? p : 0;
+      const double wf = fma(s_al[pp], vr[p], wr[p]);
+      const double dd = vr[p] * s_wc[pp] + wf * s_vc[pp];
+      s -= p < j ? dd : 0.0;
+    }
+    if (r < n) A[(size_t)c * lda + r] = s;
+    // this workgroup's x.W'(:, p) and x.v_p (rows c+2 and below), slots p and NB + p
+    const double x = r >= c + 2 && r < n ? s : 0.0;
+    const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
+#pragma unroll
+    for (int g = 0; g < 2 * kTrdNB / 8; ++g) {
+      if (8 * (g % (kTrdNB / 8)) >= j) continue;  // slots of panel columns not yet reduced
+      double pv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int slot = 8 * g + q;
+        const int p = slot < kTrdNB ? slot : slot - kTrdNB;
+        pv[q] = p < j ? x * (slot < kTrdNB ? wr[p] : vr[p]) : 0.0;
       }
-      A[(size_t)c * lda + r] = s;
+      const double t = reduce_scatter8(pv, b5, b4, b3);
+      if ((lane & 7) == 0) ured[w][8 * g + 4 * b5 + 2 * b4 + b3] = t;
     }
   }
-  const double ss = block_sum(r >= c + 2 && r < n ? s * s : 0.0, red);
-  if (threadIdx.x == 0) ws.sspart[blockIdx.x] = ss;
+  const double ss = block_sum(r >= c + 2 && r < n ? s * s : 0.0, red);  // (its barriers order ured)
+  if (tid == 0) ws.sspart[blockIdx.x] = ss;
+  if (j > 0 && tid < 2 * kTrdNB)
+    ws.upart[(size_t)blockIdx.x * 2 * kTrdNB + tid] = ured[0][tid] + ured[1][tid] + ured[2][tid] + ured[3][tid];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int last = __hip_atomic_fetch_add(ws.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
@@ -170,64 +186,64 @@ k_trd_colref(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, i
     s_last = last;
   }
   __syncthreads();
-  if (!s_last || threadIdx.x >= 64) return;
-  double xn2 = 0.0;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += 64) xn2 += __builtin_nontemporal_load(ws.sspart + b);
-  xn2 = wave_sum0(xn2);
-  if (threadIdx.x != 0) return;
+  if (!s_last) return;
+  // the last workgroup: its four waves sum the dot products' partials (slot = lane, a quarter of
+  // the workgroups each), wave 0 forms beta, tau, scale (every lane the same) and u2', u3
+  const int G = (int)gridDim.x;
   const double* col = A + (size_t)c * lda;
-  const double alpha = __builtin_nontemporal_load(col + c + 1);
+  const int p = lane < kTrdNB ? lane : lane - kTrdNB;
+  // wave 0's own operands first, in flight under the partial sums
+  double xn2 = 0.0, alpha = 0.0, dcc = 0.0, lead = 0.0;
+  if (w == 0) {
+    for (int b = lane; b < G; b += 64) xn2 += __builtin_nontemporal_load(ws.sspart + b);
+    alpha = __builtin_nontemporal_load(col + c + 1);
+    dcc = __builtin_nontemporal_load(col + c);
+    if (p < j) lead = lane < kTrdNB ? W[(size_t)p * ldw + (c + 1 - i)] : A[(size_t)(i + p) * lda + c + 1];
+  }
+  if (j > 0) {
+    double us = 0.0;
+    for (int b0 = w; b0 < G; b0 += 4 * 16) {
+      double xs[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int b = b0 + 4 * q;
+        xs[q] = b < G ? __builtin_nontemporal_load(ws.upart + (size_t)b * 2 * kTrdNB + lane) : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) us += xs[q];
+    }
+    ured[w][lane] = us;
+  }
+  __syncthreads();
+  if (tid >= 64) return;
+  xn2 = wave_sum0(xn2);
   double t = 0.0, beta = alpha, scale = 1.0;
   if (xn2 > 0.0) {
     beta = -std::copysign(std::sqrt(alpha * alpha + xn2), alpha);
     t = (beta - alpha) / beta;
     scale = 1.0 / (alpha - beta);
   }
-  d[c] = __builtin_nontemporal_load(col + c);
-  e[c] = beta;
-  tau[c] = t;
-  *ws.scale = scale;
-  *ws.cnt = 0;
-}
-
-// 2. reflector H = I - tau v v^T with H (alpha, x)^T = (beta, 0); alpha = A(c+1, c), x = A(c+2:n, c)
-__global__ void __launch_bounds__(1024)
-k_trd_larfg(double* __restrict__ A, int lda, int n, int c, double* __restrict__ d, double* __restrict__ e,
-            double* __restrict__ tau, double* __restrict__ ws_scale) {
-  __shared__ double red[16];
-  __shared__ double s_scale;
-  double* col = A + (size_t)c * lda;
-  double ss = 0.0;
-  for (int r = c + 2 + (int)threadIdx.x; r < n; r += 1024) ss = fma(col[r], col[r], ss);
-  const double xn2 = block_sum(ss, red);
-  if (threadIdx.x == 0) {
-    const double alpha = col[c + 1];
-    double t = 0.0, beta = alpha, scale = 1.0;
-    if (xn2 > 0.0) {
-      beta = -std::copysign(std::sqrt(alpha * alpha + xn2), alpha);
-      t = (beta - alpha) / beta;
-      scale = 1.0 / (alpha - beta);
-    }
-    d[c] = col[c];
+  // lane = slot: u2'[p] = scale sum x.W'(:, p) + W'(c+1-i, p), u3[p] = scale sum x.v_p + A(c+1, i+p)
+  if (p < j) {
+    const double us = ured[0][lane] + ured[1][lane] + ured[2][lane] + ured[3][lane];
+    ws.u[lane] = fma(scale, us, lead);
+  }
+  if (lane == 0) {
+    d[c] = dcc;
     e[c] = beta;
     tau[c] = t;
-    col[c + 1] = 1.0;
-    s_scale = scale;
+    *ws.scale = scale;
+    *ws.cnt = 0;
   }
-  __syncthreads();
-  const double scale = s_scale;
-  for (int r = c + 2 + (int)threadIdx.x; r < n; r += 1024) col[r] *= scale;
-  if (threadIdx.x == 0) *ws_scale = 1.0;
 }
 
 // 3. y = S v for the trailing block S = A(o:o+m, o:o+m) (lower triangle valid), v = A(o:o+m, c):
 // one workgroup per tile (I, J), I >= J, of 64 x 64; wave w takes columns 16 w .. 16 w + 15, lane l
 // row l.  Direct part -> partial[I][J], transposed part (I > J) -> partial[J][I]; the diagonal
 // tile's two halves are summed in the workgroup.  Transposed column sums by a butterfly reduce-
-// scatter over the wave (as k_symv).  The diagonal tiles also leave the block's share of the
-// dot products u2' = W'^T v and u3 = V^T v (panel columns 0 .. j) in dpart[I].
+// scatter over the wave (as k_symv).
 __global__ void __launch_bounds__(256)
-k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int j, int o, int m, int c, int nbk) {
+k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int o, int m, int c, int nbk) {
   constexpr int BS = kTrdBS, CW = BS / 4;
   // blockIdx.x -> (I, J), J <= I, row-major over the lower triangle
   const int t = (int)blockIdx.x;
@@ -239,6 +255,10 @@ k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int 
   __shared__ double red[4][BS];
   __shared__ double tr[BS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row = I * BS + lane;
+  const bool rv = row < m;
+  const bool diag = I == J;
+  const double* base = A + (size_t)(o + J * BS) * lda + o + I * BS + lane;
   const double* col = A + (size_t)c * lda;
   if (tid < BS) {
     const double scale = *ws.scale;
@@ -247,11 +267,7 @@ k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int 
     vs[1][tid] = ri < m ? refl_v(col, o + ri, c, scale) : 0.0;
   }
   __syncthreads();
-  const int row = I * BS + lane;
-  const bool rv = row < m;
-  const bool diag = I == J;
   const double vi = vs[1][lane];
-  const double* base = A + (size_t)(o + J * BS) * lda + o + I * BS + lane;
   double a = 0.0;
   const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
 #pragma unroll 1
@@ -275,27 +291,6 @@ k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int 
     if ((lane & 7) == 0) tr[w * CW + c0 + 4 * b5 + 2 * b4 + b3] = s;
   }
   red[w][lane] = a;
-  if (diag && j > 0) {
-    // wave w: dots q = 16 w .. 16 w + 15 (q < j: W', else V), loads first, then two reduce-scatters
-    const int r = o + row;  // global row
-    double x[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int q = w * 16 + k;
-      x[k] = (!rv || q >= 2 * j) ? 0.0
-             : q < j             ? ws.W[(size_t)q * ldw + (r - i)]
-                                 : A[(size_t)(i + q - j) * lda + r];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      double p[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) p[q] = x[8 * h + q] * vi;
-      const double s = reduce_scatter8(p, b5, b4, b3);
-      const int q = w * 16 + 8 * h + 4 * b5 + 2 * b4 + b3;
-      if ((lane & 7) == 0 && q < 2 * j) ws.dpart[(size_t)I * 2 * kTrdNB + q] = s;
-    }
-  }
   __syncthreads();
   if (tid < BS) {
     double s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
@@ -311,50 +306,52 @@ k_trd_symv(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int i, int 
 }
 
 // 4. W'(r - i, j) = tau (y(r) - sum_p A(r, i+p) u2[p] + W(r - i, p) u3[p]), rows of block B =
-// blockIdx.x; y from the symv partials, u2 = u2' + alpha u3 from the diagonal tiles' partials.
-// Leaves the block's W'(:, j).v in apart[B].  512 threads: 8 waves split the partials and the panel.
-__global__ void __launch_bounds__(512)
+// blockIdx.x; y from the symv partials, u2 = u2' + alpha u3.  Leaves the block's W'(:, j).v in
+// apart[B].  1024 threads: 16 waves split the partials (16 loads per lane in flight at 2^14) and
+// the panel.
+__global__ void __launch_bounds__(1024)
 k_trd_wfin(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int c, int j, int nbk,
            const double* __restrict__ tau) {
-  constexpr int BS = kTrdBS;
+  constexpr int BS = kTrdBS, NW = 16;
   __shared__ double su[2 * kTrdNB];
   __shared__ double s_al[kTrdNB];
-  __shared__ double red[8][BS];
+  __shared__ double red[NW][BS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (j > 0) {
-    const int q = tid >> 3, sub = tid & 7;
-    double s = 0.0;
-    if (q < 2 * j)
-#pragma unroll 8
-      for (int k = sub; k < nbk; k += 8) s += ws.dpart[(size_t)k * 2 * kTrdNB + q];
-    s += __shfl_xor(s, 4, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 1, 64);
-    if (sub == 0 && q < 2 * j) su[q] = s;
-    if (tid < j) s_al[tid] = ws.alpha[tid];
-    __syncthreads();
-    if (tid < j) su[tid] = fma(s_al[tid], su[j + tid], su[tid]);
-    __syncthreads();
-  }
   const int o = c + 1;
   const int B = blockIdx.x;
   const int r = o + B * BS + lane;
   const bool live = r < n;
+  double* col = A + (size_t)c * lda;
+  // the epilogue's operands, early
+  double t_c = 0.0, vr_c = 0.0;
+  if (tid < BS) {
+    t_c = tau[c];
+    vr_c = live ? refl_v(col, r, c, *ws.scale) : 0.0;
+  }
+  if (j > 0) {
+    if (tid < j) {
+      const double al = ws.alpha[tid], u3 = ws.u[kTrdNB + tid];
+      s_al[tid] = al;
+      su[tid] = fma(al, u3, ws.u[tid]);
+      su[j + tid] = u3;
+    }
+    __syncthreads();
+  }
   double y = 0.0;
   if (live) {
     const double* pp = ws.partial + (size_t)B * nbk * BS + lane;
-    int k = w;
-    for (; k + 24 < nbk; k += 32) {
-      const double p0 = pp[(size_t)k * BS], p1 = pp[(size_t)(k + 8) * BS], p2 = pp[(size_t)(k + 16) * BS],
-                   p3 = pp[(size_t)(k + 24) * BS];
-      y += p0;
-      y += p1;
-      y += p2;
-      y += p3;
+    for (int k0 = 0; k0 < nbk; k0 += NW * 16) {
+      double x[16];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int k = k0 + w + NW * t;
+        x[t] = k < nbk ? pp[(size_t)k * BS] : 0.0;
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t) y += x[t];
     }
-    for (; k < nbk; k += 8) y += pp[(size_t)k * BS];
-#pragma unroll 4
-    for (int p = w; p < j; p += 8) {
+#pragma unroll 2
+    for (int p = w; p < j; p += NW) {
       const double vr = A[(size_t)(i + p) * lda + r];
       const double wr = fma(s_al[p], vr, ws.W[(size_t)p * ldw + (r - i)]);
       y -= vr * su[p] + wr * su[j + p];
@@ -365,15 +362,13 @@ k_trd_wfin(double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int i, int
   if (tid < BS) {
     double s = red[0][tid];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) s += red[q][tid];
-    const double wv = tau[c] * s;
+    for (int q = 1; q < NW; ++q) s += red[q][tid];
+    const double wv = t_c * s;
     double prod = 0.0;
     if (live) {
       ws.W[(size_t)j * ldw + (r - i)] = wv;
-      double* col = A + (size_t)c * lda;
-      const double v = refl_v(col, r, c, *ws.scale);
-      col[r] = v;
-      prod = wv * v;
+      col[r] = vr_c;
+      prod = wv * vr_c;
     }
     prod = wave_sum0(prod);
     if (tid == 0) ws.apart[B] = prod;
@@ -423,15 +418,16 @@ __global__ void k_orm_sdiag(double* __restrict__ S, int k, const double* __restr
 }
 
 TrdWs carve(double* work, int n) {
-  const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS;
+  const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS, ng = ((size_t)n + kTrdRows - 1) / kTrdRows;
   TrdWs ws;
   ws.W = work;
   ws.partial = ws.W + (size_t)n * kTrdNB;
-  ws.dpart = ws.partial + nbk * nbk * kTrdBS;
-  ws.apart = ws.dpart + nbk * 2 * kTrdNB;
+  ws.upart = ws.partial + nbk * nbk * kTrdBS;
+  ws.u = ws.upart + ng * 2 * kTrdNB;
+  ws.apart = ws.u + 2 * kTrdNB;
   ws.alpha = ws.apart + nbk;
   ws.sspart = ws.alpha + kTrdNB;
-  ws.scale = ws.sspart + (n + 255) / 256;
+  ws.scale = ws.sspart + ng;
   ws.cnt = reinterpret_cast<int*>(ws.scale + 1);
   return ws;
 }
@@ -439,9 +435,8 @@ TrdWs carve(double* work, int n) {
 }  // namespace
 
 size_t sytrd_workspace(int n) {
-  const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS;
-  const size_t trd =
-      (size_t)n * kTrdNB + nbk * nbk * kTrdBS + nbk * 2 * kTrdNB + nbk + kTrdNB + ((size_t)n + 255) / 256 + 2;
+  const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS, ng = ((size_t)n + kTrdRows - 1) / kTrdRows;
+  const size_t trd = (size_t)n * kTrdNB + nbk * nbk * kTrdBS + ng * 2 * kTrdNB + 2 * kTrdNB + nbk + kTrdNB + ng + 2;
   const size_t orm = 2 * (size_t)n * kOrmKB + (size_t)kOrmKB * kOrmKB;  // Vb, Wt, S
   return std::max(trd, orm) * sizeof(double);
 }
@@ -477,7 +472,7 @@ int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int ld
 }
 
 int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* d, double* e, double* tau,
-                double* work, int fused) {
+                double* work) {
   const TrdWs ws = carve(work, n);
   const int ldw = n;
   if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
@@ -486,20 +481,12 @@ int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, dou
     int nbk_prev = 0;
     for (int j = 0; j < kTrdNB; ++j) {
       const int c = i + j;
-      if (fused) {
-        hipLaunchKernelGGL(k_trd_colref, dim3((n - c + 255) / 256), dim3(256), 0, st, A, lda, ws, ldw, n, i, c, j, d,
-                           e, tau, nbk_prev);
-      } else {
-        if (j > 0)
-          hipLaunchKernelGGL(k_trd_colupd, dim3((n - c + 255) / 256), dim3(256), 0, st, A, lda, ws, ldw, n, i, c, j,
-                             tau, nbk_prev);
-        hipLaunchKernelGGL(k_trd_larfg, dim3(1), dim3(1024), 0, st, A, lda, n, c, d, e, tau, ws.scale);
-      }
+      hipLaunchKernelGGL(k_trd_colref, dim3((n - c + kTrdRows - 1) / kTrdRows), dim3(kTrdRows), 0, st, A, lda, ws,
+                         ldw, n, i, c, j, d, e, tau, nbk_prev);
       const int o = c + 1, m = n - o;
       const int nbk = (m + kTrdBS - 1) / kTrdBS;
-      hipLaunchKernelGGL(k_trd_symv, dim3(nbk * (nbk + 1) / 2), dim3(256), 0, st, A, lda, ws, ldw, i, j, o, m, c,
-                         nbk);
-      hipLaunchKernelGGL(k_trd_wfin, dim3(nbk), dim3(512), 0, st, A, lda, ws, ldw, n, i, c, j, nbk, tau);
+      hipLaunchKernelGGL(k_trd_symv, dim3(nbk * (nbk + 1) / 2), dim3(256), 0, st, A, lda, ws, o, m, c, nbk);
+      hipLaunchKernelGGL(k_trd_wfin, dim3(nbk), dim3(1024), 0, st, A, lda, ws, ldw, n, i, c, j, nbk, tau);
       nbk_prev = nbk;
     }
     const int nt = n - i - kTrdNB;
@@ -522,10 +509,9 @@ int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, dou
 int eig_sym_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
                   double* e, double* tau, double* work, int* info) {
   // below 2^13 rocSOLVER's tridiagonalisation is the faster one (per-column launch latency
-  // outweighs the halved reads: 101 vs 112 ms at 2^12, profiles/r03/sytrd_probe.jsonl); the
-  // fused column kernel pays its cross-XCD release only where the columns are long
+  // outweighs the halved reads: 101 vs 112 ms at 2^12, profiles/r03/sytrd_probe.jsonl)
   if (n >= kHalfTrdMinDim) {
-    const int rc = sytrd_lower(h, st, n, A, lda, lam, e, tau, work, n >= 16384 ? 1 : 0);
+    const int rc = sytrd_lower(h, st, n, A, lda, lam, e, tau, work);
     if (rc) return rc;
   } else if (rocsolver_dsytrd(h, rocblas_fill_lower, n, A, lda, lam, e, tau) != rocblas_status_success) {
     return -3;

@@ -135,7 +135,6 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 2; ++rep) {
     timed("rocsolver_dsytrd", [&] { return (int)rocsolver_dsytrd(h, rocblas_fill_lower, n, A, n, lam, e, tau); });
     timed("sytrd_lower", [&] { return dse::sytrd_lower(h, st, n, A, n, lam, e, tau, work); });
-    timed("sytrd_lower_unfused", [&] { return dse::sytrd_lower(h, st, n, A, n, lam, e, tau, work, 0); });
     timed("rocsolver_dsyevd", [&] {
       return (int)rocsolver_dsyevd(h, rocblas_evect_original, rocblas_fill_lower, n, A, n, lref, e, info);
     });
