@@ -1756,20 +1756,30 @@ bool dense_eligible(const HostProblem& P) {
   return true;
 }
 
+// eig_impl 1 from 2^11 amplitudes: eig_sym_lower (rocSOLVER's tridiagonalisation below 2^13, the
+// half-matrix one above; dstedc; the 256-reflector back-transformation) against dsyevd measured
+// 0.46 vs 0.68 s at 2^13, 2.35 vs 4.12 s at 2^14 (profiles/r03/sytrd_probe.jsonl,
+// profiles/r03/ab/sytrd_column_kernels_ab.jsonl)
+constexpr size_t kEigHalfMinDim = 2048;
+
 // Seconds of device time, by the measured rates: the Chebyshev propagator at ~15 TF/s of its
 // algorithmic FP64 work (the N = 14 bench runs at 16.5 chip-level) with ~25 extra terms per
-// output interval, against one eigendecomposition (dsyevd on MI355X, profiles/r03/probe.jsonl:
-// 0.15 / 0.68 / 4.1 s at dim 4096 / 8192 / 16384, 3 ms for 39 registers of dim 128 together:
-// 6.4e-13 dim^3 + 4.9e-9 dim^2, + 20 ms from dim 1024 up) plus the Psi' GEMM at ~40 TF/s and the
-// observable pass.  The long reference grid (30 s, 20 000 outputs) goes dense at every register
-// size; the 1 ms head-to-head grid at N = 14 and config 2 (N = 12, 2 ms) stay on Chebyshev.
-bool dense_cheaper(const HostProblem& P, const double* t, int n_t) {
+// output interval, against one eigendecomposition plus the Psi' GEMM at ~40 TF/s and the
+// observable pass.  The eigendecomposition: dsyevd (profiles/r03/probe.jsonl: 0.15 / 0.68 / 4.1 s
+// at dim 4096 / 8192 / 16384, 3 ms for 39 registers of dim 128 together: 6.4e-13 dim^3 + 4.9e-9
+// dim^2, + 20 ms from dim 1024 up), or with eig_impl from 2^11 eig_sym_lower (0.13 / 0.46 / 2.35
+// s: 2.96e-13 dim^3 + 3.73e-9 dim^2 + 0.047).  The long reference grid (30 s, 20 000 outputs)
+// goes dense at every register size; the 1 ms head-to-head grid at N = 14 and config 2 (N = 12,
+// 2 ms) stay on Chebyshev.
+bool dense_cheaper(const HostProblem& P, const double* t, int n_t, bool half_eig) {
   if (n_t < 2) return false;
   const double dim = std::ldexp(1.0, P.n_local);
   const double alpha = 0.5 * (P.e_max - P.e_min);
   const double terms = alpha * (t[n_t - 1] - t[0]) + 25.0 * (n_t - 1);
   const double cheb = terms * dim * (P.flops_per_amp > 0 ? P.flops_per_amp : 300.0) / 15e12;
-  const double eig = 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
+  const double eig = half_eig && dim >= (double)kEigHalfMinDim
+                         ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
+                         : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
   const double dense = eig + 4.0 * dim * dim * n_t / 40e12 + (double)n_t * dim * P.n_local * 32.0 / 2e12;
   return dense < cheb;
 }
@@ -1795,10 +1805,6 @@ struct DevArena {  // device allocations of one dense_run, freed on every exit p
 // (registers of one size) of a round is built, then all its eigendecompositions run on up to
 // eig_streams solver streams at once (largest first, across sizes), then the output GEMMs.
 // Blocking; writes obs_out.
-// eig_impl 1 from 2^11 amplitudes: eig_sym_lower (rocSOLVER's tridiagonalisation below 2^13, the
-// half-matrix one above; dstedc; the 256-reflector back-transformation) against dsyevd measured
-// 0.47 vs 0.68 s at 2^13, 2.43 vs 4.12 s at 2^14 (profiles/r03/sytrd_probe.jsonl)
-constexpr size_t kEigHalfMinDim = 2048;
 
 struct DenseJob {
   int n = 0, cnt = 0, TB = 1;
@@ -2395,7 +2401,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // dense engine first (option "dense"): a register it takes is off every Chebyshev path
   bool any_small = false, any_big = false, any_dense = false;
   for (auto& P : ctx->probs) {
-    P.dn = ctx->dense && dense_eligible(P) && (ctx->dense == 2 || dense_cheaper(P, t, n_t));
+    P.dn = ctx->dense && dense_eligible(P) && (ctx->dense == 2 || dense_cheaper(P, t, n_t, ctx->eig_impl != 0));
     any_dense = any_dense || P.dn;
   }
   for (auto& P : ctx->probs) {
