@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 8
+#define DSE_ABI_VERSION 9
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -97,7 +97,8 @@ typedef struct dse_stats {
                               /* cross-tile hand-off timed out (device shared with other work)  */
   int32_t dense_problems;     /* problems this call ran on the dense eigen-propagator engine    */
                               /* (option "dense")                           */
-  int32_t reserved0;
+  int32_t span_problems;      /* registers this call ran spread over 2^s workgroups (k_span,  */
+                              /* option "span"; ABI 9)                                          */
   double dense_ms;            /* host wall time of the dense engine (all of its device work)    */
   double dense_eig_ms;        /* of which the eigendecompositions (rocSOLVER dsyevd)            */
   double exchange_ms;         /* partitioned registers over processes: time of the exchanges    */

@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 8
+DSE_ABI_VERSION = 9
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -58,7 +58,7 @@ class DseStats(C.Structure):
         ("outputs_per_launch", C.c_int32),
         ("handoff_fallbacks", C.c_int32),
         ("dense_problems", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("span_problems", C.c_int32),
         ("dense_ms", C.c_double),
         ("dense_eig_ms", C.c_double),
         ("exchange_ms", C.c_double),

@@ -112,6 +112,47 @@ struct DevProb {
   int xacc_q;             // 0, or n_acc - 1: intermediate outputs per launch-parity set
 };
 
+// ---- spanning registers (dse_span.hip): one register over 2^s cooperating workgroups ----------
+// A register of n qubits is cut into 2^s tiles of L = n - s bits (the top s qubits index the
+// tile), one workgroup per tile and compute unit, so one register's Chebyshev chain runs on 2^s
+// CUs.  In a tile, thread t of NT = 2^(L - RB) owns the R = 2^RB amplitudes x = r * NT + t.
+constexpr int kSpanMaxTop = 4;   // top (tile-index) bits: up to 16 workgroups per register
+constexpr int kSpanWaves = 16;   // hand-off flags per tile: one per wave (<= 1024 threads)
+constexpr int kSpanMaxIt = 160;  // fused-loop iteration rows (dv2): TB x (4 + pairs per iteration)
+constexpr int kSpanMaxOps = kSpanMaxTop + kSpanMaxTop * (kSpanMaxTop - 1) / 2;
+// One cross-tile operand of every tile's H application (phase 4 of k_span):
+//   kind 0  u_b of the partner h ^ e_b (its slot b): flip_b w + sum_j g_jb [x_j == h_b] w(x ^ e_j)
+//   kind 1  the partner's raw w_{k-1} under the drive flip of top bit b (no crossing pairs)
+//   kind 2  the raw w_{k-1} of the partner h ^ e_b ^ e_b2: pair (b, b2), applies iff h_b == h_b2
+struct alignas(16) SpanOp {
+  int kind, b, b2;
+  uint32_t pmask;  // partner tile = h ^ pmask
+  double c[4];     // kind 1: re0 im0 re1 im1 (by this tile's bit b); kind 2: c[0] = g
+};
+struct alignas(16) SpanTab {
+  double rr_g[6];                   // pairs among register bits (rr_index order)
+  double rflip[4][4];               // drive flips on register bits (re0 im0 re1 im1)
+  double ug[kSpanMaxTop][16];       // u pre-pass: g_{j,b} for tile bits j < L
+  double uflip[kSpanMaxTop][4];     // drive flip of top bit b
+  SpanOp ops[kSpanMaxOps];
+  int rflip_mask, u_mask, n_ops, need_raw;  // need_raw: some operand reads a partner's raw w
+  int n_it, pad[3];
+  // iteration j (thread bit j): [0] re0 im0, [1] re1 im1 (drive of j by output value t_j),
+  // [2] [3] pairs (j, register bit 0..3), [4 + q] thread pair q of the iteration (mask bits, g)
+  double2 it[kSpanMaxIt];
+};
+struct SpanDesc {
+  const SpanTab* tab;
+  double2* slots;  // [2^s tiles][s + 1 operand kinds: u_0..u_{s-1}, raw][kXSlots][2^L]
+  int* flags;      // [2^s tiles][kSpanWaves]: last term each wave of the tile published
+  int s, L;
+};
+hipError_t launch_span(int L, int RB, bool imag, const DevProb* probs, const SpanDesc* sdesc,
+                       const int2* items, int n_items, int q, int set, int n_out, int* err,
+                       hipStream_t st);
+bool span_supported(int L, int RB);
+hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu);
+
 // Coefficient row of output j of offset set `set`: kcap1 + 1 entries, row[0].x = the degree d of
 // that output's series, row[1 + k] = a_k for k = 0..d (zero beyond): 16 B per term.
 __host__ __device__ __forceinline__ const double2* coef_row(const DevProb& P, int set, int j) {

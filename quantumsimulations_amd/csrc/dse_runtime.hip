@@ -90,6 +90,9 @@ struct HostProblem {
   double2* sm_coef = nullptr;  // into dse_ctx::d_sm_coef
   int* sm_deg = nullptr;
   int final_bsel = 0;        // buffer holding the final state after dse_evolve
+  // spanning register (dse_span.hip): this evolve runs the register over 2^span_s workgroups of
+  // 2^(n - span_s) amplitudes (0: not spanned)
+  int span_s = 0;
 };
 
 // One stream's share of the problems, grouped by tile size.
@@ -103,6 +106,10 @@ struct LaneGroup {
   std::vector<int> active;     // active[k] = items with degree >= k (prefix of the group)
   std::vector<double> bytes;   // bytes[k] = algorithmic HBM bytes of the term-k launch
   std::vector<double> flops;   // flops[k] = algorithmic flops of the term-k launch
+  // spanning registers (tiles < 0): k_span<span_L, span_rb> over span_count launch items from
+  // span_off in dse_ctx::d_span_items (tiles of one register 8 apart, padding items x = -1)
+  int span_L = 0, span_rb = 0;
+  int64_t span_off = 0, span_count = 0;
 };
 struct Lane {
   hipStream_t stream = nullptr;
@@ -218,6 +225,22 @@ struct dse_ctx {
   // option "symv_fused": each product's reduction inside the product's launch (agent-scope counters
   // with a release per workgroup): measured 22.9 vs 10.4 ms for config 2, so off by default
   int symv_fused = 0;
+
+  // spanning registers (dse_span.hip): option "span" 0 off; s = 1..4: every register that fits
+  // runs over 2^s workgroups (one per CU) of 2^(n - s) amplitudes; "span_rb": amplitudes per
+  // thread 2^span_rb (0: 512 threads per workgroup)
+  int span = 0;
+  int span_rb = 0;
+  SpanDesc* d_span = nullptr;       // per problem
+  size_t span_cap = 0;
+  unsigned char* d_span_tab = nullptr;
+  size_t span_tab_cap = 0;
+  double2* d_span_slots = nullptr;  // hand-off slots of the spanned registers
+  size_t span_slot_cap = 0;         // in amplitudes
+  int* d_span_flags = nullptr;
+  size_t span_flag_cap = 0;
+  int2* d_span_items = nullptr;
+  size_t span_items_cap = 0;
 
   hipStream_t dense_stream = nullptr;
   rocblas_handle blas = nullptr;
@@ -396,6 +419,12 @@ void free_device(dse_ctx* ctx) {
   ctx->xslot_cap = 0;
   if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
   ctx->xacc_cap = 0;
+  if (ctx->d_span) (void)hipFree(ctx->d_span), ctx->d_span = nullptr;
+  if (ctx->d_span_tab) (void)hipFree(ctx->d_span_tab), ctx->d_span_tab = nullptr;
+  if (ctx->d_span_slots) (void)hipFree(ctx->d_span_slots), ctx->d_span_slots = nullptr;
+  if (ctx->d_span_flags) (void)hipFree(ctx->d_span_flags), ctx->d_span_flags = nullptr;
+  if (ctx->d_span_items) (void)hipFree(ctx->d_span_items), ctx->d_span_items = nullptr;
+  ctx->span_cap = ctx->span_tab_cap = ctx->span_slot_cap = ctx->span_flag_cap = ctx->span_items_cap = 0;
   if (ctx->d_coef) (void)hipFree(ctx->d_coef), ctx->d_coef = nullptr;
   if (ctx->d_sm_coef) (void)hipFree(ctx->d_sm_coef), ctx->d_sm_coef = nullptr;
   if (ctx->d_init) (void)hipFree(ctx->d_init), ctx->d_init = nullptr;
@@ -1316,6 +1345,12 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     HIPC(set_spin_limit((int)value));
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
+  } else if (k == "span") {  // spanning registers: 0 off, 1..4 top bits (workgroups 2^s per register)
+    if (!(value >= 0 && value <= kSpanMaxTop)) return fail(ctx, DSE_ERR_ARG, "span must be in 0..4");
+    ctx->span = (int)value;
+  } else if (k == "span_rb") {  // amplitudes per thread of k_span: 2^span_rb (0: 512 threads)
+    if (!(value >= 0 && value <= 3)) return fail(ctx, DSE_ERR_ARG, "span_rb must be in 0..3");
+    ctx->span_rb = (int)value;
   } else if (k == "mixed_launch") {
     ctx->mixed_launch = value != 0.0;
   } else if (k == "obs_overlap") {
@@ -2363,6 +2398,94 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
   return DSE_OK;
 }
 
+// ---- spanning registers (dse_span.hip) ------------------------------------------------------
+
+// amplitudes per thread of k_span for an L-bit tile: 2^rb (option span_rb, else 512 threads)
+int span_rb_for(const dse_ctx* ctx, int L) { return ctx->span_rb > 0 ? ctx->span_rb : L - 9; }
+
+bool span_eligible(const dse_ctx* ctx, const HostProblem& P, int s) {
+  if (P.side() || P.shard_bits != 0 || s < 1 || s > kSpanMaxTop) return false;
+  const int L = P.n_local - s;
+  return L >= 1 && span_supported(L, span_rb_for(ctx, L));
+}
+
+// The tables k_span reads for register P cut into 2^s tiles of L bits, RB of them register bits
+// (dse_internal.h SpanTab).  Same coefficients as build_tables, sorted by k_span's layout.
+int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
+  const int n = P.n;
+  const int TB = L - RB;
+  const int npi = (TB * (TB - 1) / 2 + TB - 1) / TB;
+  const int iw = 4 + npi;
+  if (TB * iw > kSpanMaxIt || L > 16 || RB > 4 || s > kSpanMaxTop || n != L + s) return DSE_ERR_ARG;
+  std::memset(&T, 0, sizeof(T));
+  T.n_it = TB * iw;
+  auto it = [&](int j, int e) -> double2& { return T.it[j * iw + e]; };
+  std::vector<std::pair<uint32_t, double>> tpairs;
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const double g = P.pair[i * n + j];
+      if (g == 0.0) continue;
+      if (j < TB) {
+        tpairs.push_back({(1u << i) | (1u << j), g});
+      } else if (j < L && i < TB) {
+        const int r = j - TB;
+        (r & 1 ? it(i, 2 + r / 2).y : it(i, 2 + r / 2).x) = g;
+      } else if (j < L) {
+        T.rr_g[rr_index(i - TB, j - TB)] = g;
+      } else if (i < L) {
+        T.ug[j - L][i] = g;
+        T.u_mask |= 1 << (j - L);
+      } else {
+        SpanOp& o = T.ops[T.n_ops++];
+        o.kind = 2;
+        o.b = i - L;
+        o.b2 = j - L;
+        o.pmask = (1u << o.b) | (1u << o.b2);
+        o.c[0] = g;
+        T.need_raw = 1;
+      }
+    }
+  if ((int)tpairs.size() > TB * npi) return DSE_ERR_ARG;
+  for (size_t p = 0; p < tpairs.size(); ++p) {
+    double2& e = it((int)(p / npi), 4 + (int)(p % npi));
+    e.x = __builtin_bit_cast(double, (uint64_t)tpairs[p].first);
+    e.y = tpairs[p].second;
+  }
+  for (int b = 0; b < n; ++b) {
+    double f[4];
+    for (int c = 0; c < 4; c += 2) {  // as build_tables: cos(pi/2) residues dropped
+      f[c] = P.flip[4 * b + c];
+      f[c + 1] = P.flip[4 * b + c + 1];
+      if (std::fabs(f[c]) <= 1e-15 * std::hypot(f[c], f[c + 1])) f[c] = 0.0;
+    }
+    if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
+    if (b < TB) {
+      it(b, 0) = make_double2(f[0], f[1]);
+      it(b, 1) = make_double2(f[2], f[3]);
+    } else if (b < L) {
+      for (int c = 0; c < 4; ++c) T.rflip[b - TB][c] = f[c];
+      T.rflip_mask |= 1 << (b - TB);
+    } else {
+      for (int c = 0; c < 4; ++c) T.uflip[b - L][c] = f[c];
+    }
+  }
+  // operands: u of every top bit with crossing pairs; the raw partner under the drive of every
+  // top bit without them (and with a drive)
+  for (int b = 0; b < s; ++b) {
+    const bool has_flip = T.uflip[b][0] != 0.0 || T.uflip[b][1] != 0.0 || T.uflip[b][2] != 0.0 || T.uflip[b][3] != 0.0;
+    if (!((T.u_mask >> b) & 1) && !has_flip) continue;
+    SpanOp& o = T.ops[T.n_ops++];
+    o.kind = ((T.u_mask >> b) & 1) ? 0 : 1;
+    o.b = o.b2 = b;
+    o.pmask = 1u << b;
+    if (o.kind == 1) {
+      for (int c = 0; c < 4; ++c) o.c[c] = T.uflip[b][c];
+      T.need_raw = 1;
+    }
+  }
+  return DSE_OK;
+}
+
 static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
   const auto wall0 = std::chrono::steady_clock::now();
   // DSE_HOST_TIMING=1: host time of each phase of this call on stderr (diagnostics)
@@ -2429,11 +2552,16 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   for (auto& P : ctx->probs) any_big = any_big || !P.side();
   bool persistent = ctx->persistent != 0;
   bool any_dist = false;
+  // spanning registers (option span): every register that fits runs on k_span over 2^s tiles
+  for (auto& P : ctx->probs)
+    P.span_s = (persistent && ctx->span > 0 && span_eligible(ctx, P, ctx->span)) ? ctx->span : 0;
   for (auto& P : ctx->probs) {
     if (P.side()) continue;
-    if (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0) persistent = false;
+    if (P.span_s == 0 && (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0)) persistent = false;
     any_dist = any_dist || P.dist;
   }
+  if (!persistent)
+    for (auto& P : ctx->probs) P.span_s = 0;
   // streaming: registers of more than one 2^13 tile take the Walsh-Hadamard engine (option wht)
   bool used_wht = false;
   bool any_dist_step = any_dist;  // dist shards on the step kernels: per-term shard exchange
@@ -2627,6 +2755,52 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       ctx->h_desc[pi].xslots = P.n_tiles == 2 ? ctx->d_xslots + off : nullptr;
       if (P.n_tiles == 2) off += (size_t)2 * kXSlots << P.L;
     }
+    // spanning registers: tables (one arena), descriptors, hand-off slots and flags
+    size_t slot_need = 0, flag_need = 0;
+    Arena tabs;
+    std::vector<size_t> tab_off(ctx->probs.size(), 0);
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+      const HostProblem& P = ctx->probs[pi];
+      if (!P.span_s) continue;
+      const int Ls = P.n_local - P.span_s;
+      SpanTab T;
+      if (build_span_table(P, Ls, span_rb_for(ctx, Ls), P.span_s, T) != DSE_OK)
+        return fail(ctx, DSE_ERR_ARG, "spanning-register tables do not fit (n = " + std::to_string(P.n) + ")");
+      tab_off[pi] = tabs.add(&T, sizeof(T));
+      slot_need += (size_t)(P.span_s + 1) * kXSlots << P.n_local;
+      flag_need += (size_t)kSpanWaves << P.span_s;
+    }
+    if (flag_need > 0) {
+      if ((rc = upload_arena(ctx, tabs, &ctx->d_span_tab, &ctx->span_tab_cap, ctx->lanes[0].stream))) return rc;
+      HIPC(hipStreamSynchronize(ctx->lanes[0].stream));
+      auto grow = [&](auto** ptr, size_t* cap, size_t need_bytes, const char* what) -> int {
+        if (need_bytes <= *cap) return DSE_OK;
+        if (*ptr) (void)hipFree(*ptr), *ptr = nullptr;
+        *cap = 0;
+        if (hipMalloc(ptr, need_bytes) != hipSuccess)
+          return fail(ctx, DSE_ERR_OOM, std::string(what) + " allocation failed (" + std::to_string(need_bytes) + " bytes)");
+        *cap = need_bytes;
+        return DSE_OK;
+      };
+      if ((rc = grow(&ctx->d_span_slots, &ctx->span_slot_cap, slot_need * sizeof(double2), "span slot"))) return rc;
+      if ((rc = grow(&ctx->d_span_flags, &ctx->span_flag_cap, flag_need * sizeof(int), "span flag"))) return rc;
+      if ((rc = grow(&ctx->d_span, &ctx->span_cap, ctx->probs.size() * sizeof(SpanDesc), "span descriptor"))) return rc;
+      std::vector<SpanDesc> sd(ctx->probs.size());
+      size_t so = 0, fo = 0;
+      for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+        const HostProblem& P = ctx->probs[pi];
+        std::memset(&sd[pi], 0, sizeof(SpanDesc));
+        if (!P.span_s) continue;
+        sd[pi].tab = reinterpret_cast<const SpanTab*>(ctx->d_span_tab + tab_off[pi]);
+        sd[pi].slots = ctx->d_span_slots + so;
+        sd[pi].flags = ctx->d_span_flags + fo;
+        sd[pi].s = P.span_s;
+        sd[pi].L = P.n_local - P.span_s;
+        so += (size_t)(P.span_s + 1) * kXSlots << P.n_local;
+        fo += (size_t)kSpanWaves << P.span_s;
+      }
+      HIPC(hipMemcpy(ctx->d_span, sd.data(), sd.size() * sizeof(SpanDesc), hipMemcpyHostToDevice));
+    }
   }
   HIPC(hipMemcpy(ctx->d_probs, ctx->h_desc.data(), ctx->h_desc.size() * sizeof(DevProb), hipMemcpyHostToDevice));
   // dist shards: one lane, so the RCCL exchanges are stream-ordered with every launch
@@ -2657,10 +2831,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // pair whose partner is still queued waits only for a workgroup that needs no partner.
   std::map<int, std::pair<int64_t, int64_t>> tiles_per_L;  // L -> (1-tile problems, 2-tile problems)
   for (auto& P : ctx->probs)
-    if (!P.side() && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
+    if (!P.side() && !P.span_s && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
       (P.n_tiles == 1 ? tiles_per_L[P.L].first : tiles_per_L[P.L].second) += 1;
   auto mixed_L = [&](const HostProblem& P) {
-    if (!persistent || !ctx->mixed_launch || P.side() || P.shard_bits != 0 || P.n_tiles > 2) return false;
+    if (!persistent || !ctx->mixed_launch || P.side() || P.span_s || P.shard_bits != 0 || P.n_tiles > 2) return false;
     const auto it = tiles_per_L.find(P.L);
     return it != tiles_per_L.end() && it->second.first > 0 && it->second.second > 0 &&
            2 * it->second.second <= cap;
@@ -2676,9 +2850,11 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   for (size_t i = 0; i < order.size(); ++i) {
     const HostProblem& P = ctx->probs[order[i]];
     const bool mixed = mixed_L(P);
-    const std::pair<int, int64_t> key(P.L, mixed ? 0 : P.n_tiles);  // tiles 0: a mixed group
+    // tiles 0: a mixed group; < 0: spanning registers, -(16 L_span + rb)
+    const int Ls = P.n_local - P.span_s;
+    const std::pair<int, int64_t> key(P.L, P.span_s ? -(16 * Ls + span_rb_for(ctx, Ls)) : (mixed ? 0 : P.n_tiles));
     int lane = (int)(i % n_lanes);
-    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1 || mixed) ? 0 : 1;
+    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1 || mixed || P.span_s) ? 0 : 1;
     // shards of one register read each other's vectors: same lane, hence the same launches
     if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);
@@ -2696,6 +2872,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       LaneGroup g;
       g.L = kv.first.first;
       g.tiles = (int)kv.first.second;
+      if (g.tiles < 0) g.span_L = (-g.tiles) / 16, g.span_rb = (-g.tiles) % 16;
       g.off = (int64_t)items.size();
       for (int pi : kv.second) {  // already in degree order
         ctx->item_pos[pi] = (int64_t)items.size();
@@ -2792,6 +2969,38 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
         }
       }
     HIPC(hipMemcpy(ctx->d_items_iv, iv.data(), iv.size() * sizeof(int2), hipMemcpyHostToDevice));
+    // spanning groups: launch items (problem, tile); the tiles of one register 8 items apart, so
+    // under the round-robin dispatch of workgroups to the 8 XCDs they share one XCD's L2 (speed
+    // only), in blocks of 8 registers padded with items x = -1 (return at once)
+    std::vector<int2> sitems;
+    for (auto& ln : ctx->lanes)
+      for (auto& g : ln.groups) {
+        if (g.tiles >= 0) continue;
+        std::vector<int> pis;
+        for (int64_t i = 0; i < g.count; ++i) {
+          const int2 e = items[g.off + i];
+          if (pis.empty() || pis.back() != e.x) pis.push_back(e.x);
+        }
+        g.span_off = (int64_t)sitems.size();
+        for (size_t b0 = 0; b0 < pis.size(); b0 += 8) {
+          const int s = ctx->probs[pis[b0]].span_s;
+          const size_t base = sitems.size();
+          sitems.resize(base + ((size_t)8 << s), make_int2(-1, 0));
+          for (size_t i = b0; i < std::min(pis.size(), b0 + 8); ++i)
+            for (int h = 0; h < (1 << s); ++h) sitems[base + (size_t)h * 8 + (i - b0)] = make_int2(pis[i], h);
+        }
+        g.span_count = (int64_t)sitems.size() - g.span_off;
+      }
+    if (!sitems.empty()) {
+      if (sitems.size() > ctx->span_items_cap) {
+        if (ctx->d_span_items) (void)hipFree(ctx->d_span_items), ctx->d_span_items = nullptr;
+        ctx->span_items_cap = 0;
+        if (hipMalloc(&ctx->d_span_items, sitems.size() * sizeof(int2)) != hipSuccess)
+          return fail(ctx, DSE_ERR_OOM, "span item allocation failed");
+        ctx->span_items_cap = sitems.size();
+      }
+      HIPC(hipMemcpy(ctx->d_span_items, sitems.data(), sitems.size() * sizeof(int2), hipMemcpyHostToDevice));
+    }
   }
   if (persistent) {
     const size_t need = 2 * kIvWaves * ctx->probs.size() + 1;  // flags, error word
@@ -2936,8 +3145,18 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
         const int T = 1 << g.L;
         if (persistent) {
           // all K terms of the interval in one launch; 2-tile groups in co-resident chunks
-          if (g.tiles != 1) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
-          const int64_t gcap = g.tiles == 2 ? cap : g.count;  // mixed (0): one launch, see above
+          // spanning registers: one k_span launch for the group (every register's tiles resident
+          // together: the runtime sizes span groups to the chip), flags zeroed first
+          if (g.tiles < 0) HIPC(hipMemsetAsync(ctx->d_span_flags, 0, ctx->span_flag_cap, ln.stream));
+          else if (g.tiles != 1) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
+          auto launch_g = [&](int64_t off, int cnt) -> hipError_t {
+            if (g.tiles < 0)
+              return launch_span(g.span_L, g.span_rb, imag_all, ctx->d_probs, ctx->d_span, ctx->d_span_items + g.span_off,
+                                 (int)g.span_count, q, set, G.n_out, d_err, ln.stream);
+            return launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out,
+                                   ctx->d_flags, d_err, ln.stream);
+          };
+          const int64_t gcap = g.tiles == 2 ? cap : g.count;  // mixed (0), span (< 0): one launch
           for (int64_t off = 0; off < g.count; off += gcap) {
             const int cnt = (int)std::min<int64_t>(gcap, g.count - off);
             double fl = 0.0, am = 0.0;
@@ -2949,12 +3168,12 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
             if (timed && 2 * ln.ev_used[pool] + 2 <= ln.ev[pool].size()) {
               const size_t i = ln.ev_used[pool]++;
               HIPC(hipEventRecord(ln.ev[pool][2 * i], ln.stream));
-              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out, ctx->d_flags, d_err, ln.stream));
+              HIPC(launch_g(off, cnt));
               HIPC(hipEventRecord(ln.ev[pool][2 * i + 1], ln.stream));
               pool_bytes[li * 2 + pool].push_back(fl);
               pool_amps[li * 2 + pool].push_back(am);
             } else {
-              HIPC(launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out, ctx->d_flags, d_err, ln.stream));
+              HIPC(launch_g(off, cnt));
             }
             launches += 1.0;
             amp_updates += am;
@@ -3069,6 +3288,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     int n_dense = 0;
     for (auto& P : ctx->probs) n_dense += P.dn ? 1 : 0;
     stats->dense_problems = n_dense;
+    int n_span = 0;
+    for (auto& P : ctx->probs) n_span += P.span_s ? 1 : 0;
+    stats->span_problems = n_span;
     stats->dense_ms = dense_ms;
     stats->dense_eig_ms = dense_eig_ms;
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;

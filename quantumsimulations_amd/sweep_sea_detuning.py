@@ -18,6 +18,13 @@ from .sweep import detuning_label, f1R_for_resonance  # noqa: F401
 from .sweep_runner import run_sweep_sea_detuning  # noqa: F401
 
 
+def _safe_normalized_difference(num: float, denom: float) -> float:
+    """num / denom, NaN when denom is 0 or NaN (reference sweep_sea_detuning.py:324-335)."""
+    if denom == 0.0 or np.isnan(denom):
+        return float("nan")
+    return num / denom
+
+
 def main(argv=None) -> str:
     ap = argparse.ArgumentParser(description="Sea-detuning sweep on MI355X GPUs")
     ap.add_argument("--n-sea", type=int, default=6)

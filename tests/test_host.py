@@ -338,3 +338,23 @@ def test_evolve_groups_split_by_engine_class():
     assert [engine_class(p) for p in probs] == [0, 0, 1, 0, 1, 0]
     g = evolve_groups(keys, probs)
     assert g == {(1e-3, 101, 0): [0, 1, 3], (1e-3, 101, 1): [2, 4], (2e-3, 101, 0): [5]}
+
+
+def test_root_drop_in_shims_import():
+    """The repository-root module names the reference's scripts import (`import
+    sweep_sea_detuning`, `from dipolar_ensemble_with_rare import ...`) resolve, with every name
+    the shims re-export (reference sweep_sea_detuning.py:324 `_safe_normalized_difference`)."""
+    import importlib
+    import math
+    import sys
+    sys.path.insert(0, str(ROOT))
+    try:
+        for name in ("sweep_sea_detuning", "dipolar_ensemble_with_rare"):
+            sys.modules.pop(name, None)
+            importlib.import_module(name)
+        import sweep_sea_detuning as ssd
+        assert ssd._safe_normalized_difference(1.0, 2.0) == 0.5
+        assert math.isnan(ssd._safe_normalized_difference(1.0, 0.0))
+        assert math.isnan(ssd._safe_normalized_difference(1.0, float("nan")))
+    finally:
+        sys.path.remove(str(ROOT))

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Spanning-register timings (dse_span.hip): JSON lines of wall and kernel time.
+
+    python3 tools/probe_span.py lone [reps]     one N = 14 register per evolve (center_on and
+                                                shell_off at 75 / 150 kHz), span 0 / 2 / 3 / 4
+    python3 tools/probe_span.py sweep [reps]    the bench's 192 evolutions with span 0 / 2 / 3 / 4
+    python3 tools/probe_span.py shard [reps]    one GPU's share of the 64-point sweep on 8 GPUs
+                                                (8 points = 24 evolutions), span 0 / 2 / 3 / 4
+Grid: config 3's 1 ms / 101 outputs.  Kernel time = HIP events around every interval launch.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from quantumsimulations_amd import problem as pb  # noqa: E402
+from quantumsimulations_amd.engine import Engine  # noqa: E402
+from quantumsimulations_amd.sweep import VARIANTS, sweep_params, sweep_point_params  # noqa: E402
+
+T = np.linspace(0.0, 1e-3, 101)
+
+
+def run(eng, probs, span, reps, label, **opts):
+    eng.clear()
+    eng.set_option("span", span)
+    for k, v in opts.items():
+        eng.set_option(k, v)
+    for p in probs:
+        eng.add(p)
+    eng.evolve(T)  # warm-up (tables, allocations)
+    walls, kms = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        obs, st = eng.evolve(T)
+        walls.append((time.perf_counter() - t0) * 1e3)
+        kms.append(st["step_kernel_ms"])
+    eng.set_option("span", 0)
+    eng.clear()
+    terms = st["h_applications"]
+    rec = {"case": label, "span": span, "n_probs": len(probs), "wall_ms": min(walls),
+           "wall_ms_all": [round(w, 2) for w in walls], "kernel_ms": min(kms),
+           "span_problems": st["span_problems"], "max_degree": st["max_degree"],
+           "launches": st["step_launches"], "h_applications": terms,
+           "us_per_term_chain": 1e3 * min(kms) / max(1, st["max_degree"] * st["n_intervals"] /
+                                                      max(1, st["outputs_per_launch"])),
+           "fallbacks": st["handoff_fallbacks"], **opts}
+    print(json.dumps(rec), flush=True)
+    return obs
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "lone"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    spans = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 2, 3, 4]
+    with Engine(0) as eng:
+        if what == "lone":
+            for variant in ("center_on", "shell_off"):
+                for d in (75e3, 150e3):
+                    p = pb.build_problem(sweep_point_params(13, d, variant, T[-1], len(T)))
+                    ref = None
+                    for s in spans:
+                        obs = run(eng, [p], s, reps, f"{variant}_{int(d / 1e3)}k")
+                        if ref is None:
+                            ref = obs
+                        else:
+                            print(json.dumps({"check": f"{variant}_{int(d / 1e3)}k", "span": s,
+                                              "max_abs_diff_vs_span0": float(np.max(np.abs(obs - ref)))}), flush=True)
+        else:
+            n_pts = 64 if what == "sweep" else 8
+            dets = np.linspace(0.0, 150e3, 64)
+            if what == "shard":  # rank 0 of 8 under the strong split: detunings j = 0 mod 8
+                dets = dets[0::8] if os.environ.get("SHARD_RANK") is None else dets[int(os.environ["SHARD_RANK"])::8]
+            params = sweep_params(13, dets[:n_pts], T[-1], len(T))
+            probs = [pb.build_problem(p) for p in params]
+            ref = None
+            for s in spans:
+                obs = run(eng, probs, s, reps, what)
+                if ref is None:
+                    ref = obs
+                else:
+                    print(json.dumps({"check": what, "span": s,
+                                      "max_abs_diff_vs_span0": float(np.max(np.abs(obs - ref)))}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
