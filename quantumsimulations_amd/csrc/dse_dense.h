@@ -24,6 +24,8 @@ constexpr int kDenseMaxQubits = 14;  // 2^14 x 2^14 fp64 = 2 GiB per eigenvector
 struct DenseProb {
   int n;              // qubits (engine bit order: bit b = site b)
   int rot;            // 1: drives imaginary, H' = D H D^dagger; 0: drives real, H' = H
+  int refine;         // 1: refined eigenvalues and double-double phases (option dense_refine);
+                      // 0: the eigensolver's eigenvalues, phases sincos(lam tau) in fp64
   uint64_t sea_mask;
   int rare_bit;       // -1: none in the register
   int n_sea;          // popcount(sea_mask)
@@ -34,13 +36,20 @@ struct DenseProb {
   const double* pair;   // [n * n] pair flip coefficient g_ij (i < j), applies iff bit_i == bit_j
   const double* flip;   // [4 n]   drive flip of bit b: re0 im0 re1 im1 by the output bit value
   double* V;            // [dim * dim] column-major: H' in, eigenvectors out (rocSOLVER)
-  const double* lam;    // [dim] eigenvalues (ascending)
+  double* lam;          // [dim] eigenvalues (ascending); after k_dense_rq the high part of each
+                        // refined eigenvalue (double-double lam + lam_lo)
+  double* lam_lo;       // [dim] low parts (zero without the refinement)
   double* obs;          // [n_t][8] raw observable sums of this problem (finish_obs order)
   double2* final_state; // [dim] psi(t_last) in the reference frame (dse_get_state), or null
 };
 
 // H' of every problem into its (zeroed) V
 hipError_t launch_dense_h(const DenseProb* d, int count, int dim, hipStream_t st);
+// Rayleigh-quotient refinement of every eigenvalue in double-double arithmetic: lam_a = v_a^T H' v_a
+// / v_a^T v_a with H' applied from the coefficient tables (the same fp64 matrix k_dense_h built).
+// The eigensolver's eigenvalues carry errors ~eps ||H'|| sqrt(dim) (a phase error growing like that
+// times t); the quotient of its eigenvector is exact to ~(eps ||H'||)^2 / gap + eps^2 ||H'||.
+hipError_t launch_dense_rq(const DenseProb* d, int count, int dim, hipStream_t st);
 // phase columns of output times tau[0 .. tb): P[a + j dim] = c_a cos(lambda_a tau_j),
 // P[a + (tb + j) dim] = -c_a sin(lambda_a tau_j); problem p's block at P + p * pstride
 hipError_t launch_dense_phase(const DenseProb* d, int count, int dim, const double* tau, int tb,

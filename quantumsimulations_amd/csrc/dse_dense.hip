@@ -14,6 +14,44 @@ __device__ __forceinline__ double2 ipow(int m) {
   return make_double2(m == 0 ? 1.0 : (m == 2 ? -1.0 : 0.0), m == 1 ? 1.0 : (m == 3 ? -1.0 : 0.0));
 }
 
+// Diagonal element <x|H'|x> (fp64, one fixed order: k_dense_h and k_dense_rq must agree bitwise).
+__device__ __forceinline__ double dense_diag(const DenseProb& P, uint32_t x) {
+  const int n = P.n;
+  double d = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double si = 0.5 - (double)((x >> i) & 1u);
+    d += P.field[i] * si;
+    for (int j = i + 1; j < n; ++j) d += P.zz[i * n + j] * si * (0.5 - (double)((x >> j) & 1u));
+  }
+  return d;
+}
+
+// Off-diagonal elements <y|H'|x> of column x: f(y, value) for every drive flip and pair flip.
+template <typename F>
+__device__ __forceinline__ void dense_offdiag(const DenseProb& P, uint32_t x, F&& f) {
+  const int n = P.n;
+  const int px = __popc(x);
+  for (int b = 0; b < n; ++b) {
+    const double* fl = P.flip + 4 * b;
+    if (fl[0] == 0.0 && fl[1] == 0.0 && fl[2] == 0.0 && fl[3] == 0.0) continue;
+    const uint32_t y = x ^ (1u << b);
+    const uint32_t vb = (y >> b) & 1u;  // output bit value selects the coefficient
+    const double cr = vb ? fl[2] : fl[0], ci = vb ? fl[3] : fl[1];
+    double v = cr;
+    if (P.rot) {  // i^{|y| - |x|} c, real by construction (imaginary drive)
+      const double2 ph = ipow(__popc(y) - px);
+      v = ph.x * cr - ph.y * ci;
+    }
+    f(y, v);
+  }
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const double g = P.pair[i * n + j];
+      if (g == 0.0 || (((x >> i) ^ (x >> j)) & 1u)) continue;
+      f(x ^ ((1u << i) | (1u << j)), P.rot ? -g : g);  // i^{+-2} = -1
+    }
+}
+
 // Column x of H' (rows y with <y|H'|x> != 0); V is zero on entry.  Matrix elements follow
 // dipolar_ensemble_with_rare.py:453-588 in the bitwise form of SURVEY.md Appendix A.
 __global__ void __launch_bounds__(256)
@@ -21,35 +59,96 @@ k_dense_h(const DenseProb* __restrict__ probs, int dim) {
   const DenseProb& P = probs[blockIdx.y];
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   if (x >= (uint32_t)dim) return;
-  const int n = P.n;
   double* col = P.V + (size_t)x * dim;
-  double d = 0.0;
-  for (int i = 0; i < n; ++i) {
-    const double si = 0.5 - (double)((x >> i) & 1u);
-    d += P.field[i] * si;
-    for (int j = i + 1; j < n; ++j) d += P.zz[i * n + j] * si * (0.5 - (double)((x >> j) & 1u));
+  col[x] = dense_diag(P, x);
+  dense_offdiag(P, x, [&](uint32_t y, double v) { col[y] = v; });
+}
+
+// ---- double-double arithmetic (value = hi + lo, |lo| <= ulp(hi) / 2) ----
+struct ddv {
+  double hi, lo;
+};
+__device__ __forceinline__ ddv dd_two_sum(double a, double b) {
+  const double s = a + b;
+  const double bb = s - a;
+  return {s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ ddv dd_fast(double a, double b) {  // |a| >= |b|
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+__device__ __forceinline__ ddv dd_add(ddv a, ddv b) {
+  ddv s = dd_two_sum(a.hi, b.hi);
+  s.lo += a.lo + b.lo;
+  return dd_fast(s.hi, s.lo);
+}
+__device__ __forceinline__ ddv dd_prod(double a, double b) {
+  const double p = a * b;
+  return {p, fma(a, b, -p)};
+}
+__device__ __forceinline__ ddv dd_mul_d(ddv a, double b) {
+  ddv p = dd_prod(a.hi, b);
+  p.lo = fma(a.lo, b, p.lo);
+  return dd_fast(p.hi, p.lo);
+}
+__device__ __forceinline__ ddv dd_div(ddv a, ddv b) {
+  const double q1 = a.hi / b.hi;
+  ddv r = dd_add(a, dd_mul_d(b, -q1));
+  const double q2 = r.hi / b.hi;
+  return dd_fast(q1, q2);
+}
+
+// Rayleigh quotient of eigenvector a (column a of V) in double-double: one workgroup per
+// (eigenvector, problem); thread partials summed in a fixed order (deterministic)
+__global__ void __launch_bounds__(256)
+k_dense_rq(const DenseProb* __restrict__ probs, int dim) {
+  __shared__ double red[4][256];
+  const DenseProb& P = probs[blockIdx.y];
+  const uint32_t a = blockIdx.x;
+  const double* v = P.V + (size_t)a * dim;
+  ddv num = {0.0, 0.0}, den = {0.0, 0.0};
+  for (uint32_t x = threadIdx.x; x < (uint32_t)dim; x += 256u) {
+    const double vx = v[x];
+    ddv y = dd_prod(dense_diag(P, x), vx);
+    dense_offdiag(P, x, [&](uint32_t yy, double c) { y = dd_add(y, dd_prod(c, v[yy])); });
+    num = dd_add(num, dd_mul_d(y, vx));
+    den = dd_add(den, dd_prod(vx, vx));
   }
-  col[x] = d;
-  const int px = __popc(x);
-  for (int b = 0; b < n; ++b) {
-    const double* f = P.flip + 4 * b;
-    if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
-    const uint32_t y = x ^ (1u << b);
-    const uint32_t vb = (y >> b) & 1u;  // output bit value selects the coefficient
-    const double cr = vb ? f[2] : f[0], ci = vb ? f[3] : f[1];
-    double v = cr;
-    if (P.rot) {  // i^{|y| - |x|} c, real by construction (imaginary drive)
-      const double2 ph = ipow(__popc(y) - px);
-      v = ph.x * cr - ph.y * ci;
+  const int t = threadIdx.x;
+  red[0][t] = num.hi, red[1][t] = num.lo, red[2][t] = den.hi, red[3][t] = den.lo;
+  __syncthreads();
+  if (t == 0) {
+    ddv sn = {0.0, 0.0}, sd = {0.0, 0.0};
+    for (int i = 0; i < 256; ++i) {
+      sn = dd_add(sn, ddv{red[0][i], red[1][i]});
+      sd = dd_add(sd, ddv{red[2][i], red[3][i]});
     }
-    col[y] = v;
+    const ddv lam = dd_div(sn, sd);
+    P.lam[a] = lam.hi;
+    P.lam_lo[a] = lam.lo;
   }
-  for (int i = 0; i < n; ++i)
-    for (int j = i + 1; j < n; ++j) {
-      const double g = P.pair[i * n + j];
-      if (g == 0.0 || (((x >> i) ^ (x >> j)) & 1u)) continue;
-      col[x ^ ((1u << i) | (1u << j))] = P.rot ? -g : g;  // i^{+-2} = -1
-    }
+}
+
+// cos and sin of (lam_hi + lam_lo) tau: the product in double-double, reduced modulo 2 pi with a
+// three-part 2 pi (the first part 27 significant bits, so k C1 is exact for |k| < 2^26, i.e.
+// |lam tau| < 4e8 rad), then sincos of the reduced angle's high part corrected by its low part.
+// A plain fp64 product lam * tau rounds the angle by ulp(lam tau): 1.5e-8 rad at 1.5e8 rad,
+// the reference grid's 30 s at |lam| ~ 5e6 rad/s.
+__device__ __forceinline__ void dd_sincos(double lh, double ll, double tau, double* s, double* c) {
+  constexpr double C1 = 0x1.921fb54p+2;            // 2 pi, high 27 bits
+  constexpr double C2 = 0x1.10b4611a62633p-28;     // next 53 bits
+  constexpr double C3 = 0x1.45c06e0e68948p-84;     // next 53 bits
+  constexpr double INV = 0.15915494309189533576888376337251436;
+  const ddv p = dd_mul_d(ddv{lh, ll}, tau);
+  const double k = rint(p.hi * INV);
+  ddv r = dd_two_sum(p.hi, -k * C1);  // k C1 exact
+  r = dd_add(r, dd_prod(-k, C2));
+  r.lo = fma(-k, C3, r.lo + p.lo);
+  r = dd_fast(r.hi, r.lo);
+  double sh, ch;
+  sincos(r.hi, &sh, &ch);
+  *s = fma(ch, r.lo, sh);
+  *c = fma(-sh, r.lo, ch);
 }
 
 __global__ void __launch_bounds__(256)
@@ -61,7 +160,10 @@ k_dense_phase(const DenseProb* __restrict__ probs, int dim, const double* __rest
   if (a >= (uint32_t)dim) return;
   const double c = P.V[P.x0 + (size_t)a * dim];  // <v_a | e_x0>
   double s, co;
-  sincos(P.lam[a] * tau[j], &s, &co);
+  if (P.refine)
+    dd_sincos(P.lam[a], P.lam_lo[a], tau[j], &s, &co);
+  else
+    sincos(P.lam[a] * tau[j], &s, &co);
   double* blk = Pm + blockIdx.z * pstride;
   blk[a + (size_t)j * dim] = c * co;
   blk[a + (size_t)(tb + j) * dim] = -c * s;
@@ -142,7 +244,10 @@ k_dense_final(const DenseProb* __restrict__ probs, int dim, const double* __rest
   const double* im = re + (size_t)tb * dim;
   // psi_x = exp(-i shift tau) i^{|x0| - |x|} psi'_x   (rot; psi'(0) = e_x0 stands for i^{|x0|} e_x0)
   double s, c;
-  sincos(-P.shift * tau_last, &s, &c);
+  if (P.refine)
+    dd_sincos(-P.shift, 0.0, tau_last, &s, &c);
+  else
+    sincos(-P.shift * tau_last, &s, &c);
   double2 ph = make_double2(c, s);
   if (P.rot) {
     const double2 q = ipow(__popcll(P.x0) - __popc(x));
@@ -156,6 +261,11 @@ k_dense_final(const DenseProb* __restrict__ probs, int dim, const double* __rest
 
 hipError_t launch_dense_h(const DenseProb* d, int count, int dim, hipStream_t st) {
   hipLaunchKernelGGL(k_dense_h, dim3((dim + 255) / 256, count), dim3(256), 0, st, d, dim);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_rq(const DenseProb* d, int count, int dim, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_rq, dim3(dim, count), dim3(256), 0, st, d, dim);
   return hipGetLastError();
 }
 

@@ -151,6 +151,7 @@ hipError_t launch_span(int L, int RB, bool imag, const DevProb* probs, const Spa
                        const int2* items, int n_items, int q, int set, int n_out, int* err,
                        hipStream_t st);
 bool span_supported(int L, int RB);
+hipError_t set_span_spin_limit(int limit);
 hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu);
 
 // Coefficient row of output j of offset set `set`: kcap1 + 1 entries, row[0].x = the degree d of

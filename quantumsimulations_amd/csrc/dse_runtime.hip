@@ -230,6 +230,7 @@ struct dse_ctx {
   // runs over 2^s workgroups (one per CU) of 2^(n - s) amplitudes; "span_rb": amplitudes per
   // thread 2^span_rb (0: 512 threads per workgroup)
   int span = 0;
+  int span_tile = 0;                // option "span_tile" L > 0: every register of n > L qubits spans 2^(n-L) tiles
   int span_rb = 0;
   SpanDesc* d_span = nullptr;       // per problem
   size_t span_cap = 0;
@@ -252,6 +253,10 @@ struct dse_ctx {
   // half-matrix tridiagonalisation from 2^13, rocSOLVER dstedc, the blocked back-transformation)
   // from kEigHalfMinDim amplitudes, dsyevd below; 2 eig_sym_lower from 2^10 (tests)
   int eig_impl = 1;
+  // dense engine: eigenvalues refined by double-double Rayleigh quotients and output phases reduced
+  // in double-double (option "dense_refine", default 1; 0: the eigensolver's eigenvalues and fp64
+  // phases, whose error grows like eps |lambda| t: ~1e-8 at the reference grid's 30 s)
+  int dense_refine = 1;
   std::vector<hipStream_t> eig_st;
   std::vector<rocblas_handle> eig_h;
 };
@@ -1331,6 +1336,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "eig_impl") {  // dense engine eigensolver: 0 dsyevd, 1 auto, 2 half-matrix from 2^10
     if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "eig_impl must be 0, 1 or 2");
     ctx->eig_impl = (int)value;
+  } else if (k == "dense_refine") {  // dense engine: refined eigenvalues + double-double phases
+    ctx->dense_refine = value != 0.0;
   } else if (k == "symv_fused") {  // matrix mode: each product's reduction in the product's launch
     ctx->symv_fused = value != 0.0;
   } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
@@ -1343,11 +1350,15 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     HIPC(set_handoff_fences(value != 0.0));
   } else if (k == "spin_limit") {  // diagnostics: partner-flag polls per hand-off (< 0: always fail)
     HIPC(set_spin_limit((int)value));
+    HIPC(set_span_spin_limit((int)value));
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
   } else if (k == "span") {  // spanning registers: 0 off, 1..4 top bits (workgroups 2^s per register)
     if (!(value >= 0 && value <= kSpanMaxTop)) return fail(ctx, DSE_ERR_ARG, "span must be in 0..4");
     ctx->span = (int)value;
+  } else if (k == "span_tile") {  // spanning registers: tile bits L (0 off); n > L qubits span 2^(n-L) tiles
+    if (!(value == 0 || (value >= 10 && value <= 13))) return fail(ctx, DSE_ERR_ARG, "span_tile must be 0 or in 10..13");
+    ctx->span_tile = (int)value;
   } else if (k == "span_rb") {  // amplitudes per thread of k_span: 2^span_rb (0: 512 threads)
     if (!(value >= 0 && value <= 3)) return fail(ctx, DSE_ERR_ARG, "span_rb must be in 0..3");
     ctx->span_rb = (int)value;
@@ -1846,7 +1857,7 @@ struct DenseJob {
   size_t dim = 0, pstride = 0;
   std::vector<int> list;  // problem indices
   DevArena ba;
-  double *V = nullptr, *lam = nullptr, *E = nullptr, *Pm = nullptr, *Psi = nullptr, *obs = nullptr;
+  double *V = nullptr, *lam = nullptr, *lam_lo = nullptr, *E = nullptr, *Pm = nullptr, *Psi = nullptr, *obs = nullptr;
   rocblas_int* info = nullptr;
   DenseProb* d_desc = nullptr;
 };
@@ -1906,6 +1917,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       DevArena& ba = J->ba;
       J->V = ba.get<double>(dim * dim * cnt);
       J->lam = ba.get<double>(dim * cnt);
+      J->lam_lo = ba.get<double>(dim * cnt);
       J->E = ba.get<double>(dim * cnt);
       J->info = ba.get<rocblas_int>(cnt);
       J->Pm = ba.get<double>(pstride * cnt);
@@ -1914,7 +1926,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       const size_t tsz = (size_t)(2 * n * n + 5 * n);
       double* tabs = ba.get<double>(tsz * cnt);
       J->d_desc = ba.get<DenseProb>(cnt);
-      if (!J->V || !J->lam || !J->E || !J->info || !J->Pm || !J->Psi || !J->obs || !tabs || !J->d_desc) {
+      if (!J->V || !J->lam || !J->lam_lo || !J->E || !J->info || !J->Pm || !J->Psi || !J->obs || !tabs || !J->d_desc) {
         if (!jobs.empty()) break;  // this round is full: the register waits for the next one
         return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed (dim " + std::to_string(dim) + ")");
       }
@@ -1942,6 +1954,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         D.flip = d + n + 2 * n * n;
         D.V = J->V + dim * dim * i;
         D.lam = J->lam + dim * i;
+        D.lam_lo = J->lam_lo + dim * i;
+        D.refine = ctx->dense_refine;
         D.obs = J->obs + (size_t)n_t * 8 * i;
         D.final_state = P.buf[0];
       }
@@ -2074,6 +2088,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: eigensolver did not converge (info " +
                                                     std::to_string(hinfo[i]) + ")");
       const double one = 1.0, zero = 0.0;
+      if (ctx->dense_refine) HIPC(launch_dense_rq(J.d_desc, cnt, (int)dim, st));
       for (int tb0 = 0; tb0 < n_t; tb0 += TB) {
         const int tb = std::min(TB, n_t - tb0);
         HIPC(launch_dense_phase(J.d_desc, cnt, (int)dim, d_tau + tb0, tb, J.Pm, pstride, st));
@@ -2403,6 +2418,15 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
 // amplitudes per thread of k_span for an L-bit tile: 2^rb (option span_rb, else 512 threads)
 int span_rb_for(const dse_ctx* ctx, int L) { return ctx->span_rb > 0 ? ctx->span_rb : L - 9; }
 
+bool span_eligible(const dse_ctx* ctx, const HostProblem& P, int s);
+
+// top bits a register spans in this evolve (0: not spanned): option span_tile fixes the tile,
+// option span the number of top bits
+int span_bits(const dse_ctx* ctx, const HostProblem& P) {
+  const int s = ctx->span_tile > 0 ? P.n_local - ctx->span_tile : ctx->span;
+  return span_eligible(ctx, P, s) ? s : 0;
+}
+
 bool span_eligible(const dse_ctx* ctx, const HostProblem& P, int s) {
   if (P.side() || P.shard_bits != 0 || s < 1 || s > kSpanMaxTop) return false;
   const int L = P.n_local - s;
@@ -2554,7 +2578,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   bool any_dist = false;
   // spanning registers (option span): every register that fits runs on k_span over 2^s tiles
   for (auto& P : ctx->probs)
-    P.span_s = (persistent && ctx->span > 0 && span_eligible(ctx, P, ctx->span)) ? ctx->span : 0;
+    P.span_s = persistent ? span_bits(ctx, P) : 0;
   for (auto& P : ctx->probs) {
     if (P.side()) continue;
     if (P.span_s == 0 && (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0)) persistent = false;
@@ -2983,11 +3007,13 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
         }
         g.span_off = (int64_t)sitems.size();
         for (size_t b0 = 0; b0 < pis.size(); b0 += 8) {
-          const int s = ctx->probs[pis[b0]].span_s;
+          int s = 0;  // the block's widest register sets its size (span_tile mixes 13 and 14 qubits)
+          for (size_t i = b0; i < std::min(pis.size(), b0 + 8); ++i) s = std::max(s, ctx->probs[pis[i]].span_s);
           const size_t base = sitems.size();
           sitems.resize(base + ((size_t)8 << s), make_int2(-1, 0));
           for (size_t i = b0; i < std::min(pis.size(), b0 + 8); ++i)
-            for (int h = 0; h < (1 << s); ++h) sitems[base + (size_t)h * 8 + (i - b0)] = make_int2(pis[i], h);
+            for (int h = 0; h < (1 << ctx->probs[pis[i]].span_s); ++h)
+              sitems[base + (size_t)h * 8 + (i - b0)] = make_int2(pis[i], h);
         }
         g.span_count = (int64_t)sitems.size() - g.span_off;
       }

@@ -35,6 +35,14 @@
 
 namespace dse {
 
+// Polls of the partners' flags before a hand-off is declared failed (s_sleep 1 between polls);
+// negative: fail at once (diagnostics: exercises the fallback)
+__device__ int g_span_spin_limit = 1 << 22;
+
+hipError_t set_span_spin_limit(int limit) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_span_spin_limit), &limit, sizeof(int));
+}
+
 namespace {
 
 typedef __attribute__((address_space(1))) int gint;
@@ -98,6 +106,8 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
        const int2* __restrict__ items, int q, int set, int n_out, int* __restrict__ err) {
   using G = SpanGeo<L, RB>;
   constexpr int R = G::R, TB = G::TB, NT = G::NT, IW = G::IW, NPI = G::NPI, US = G::US;
+  constexpr int NB = R <= 4 ? 4 : 3;         // operands loaded together in phase 4
+  constexpr int J_PUB = TB > 2 ? 2 : TB - 1;  // loop iteration that publishes the term
   constexpr uint32_t TBYTES = G::TBYTES;
   __shared__ SpanShared<L, RB> S;
 
@@ -163,6 +173,17 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
     }
   }
   __syncthreads();
+
+  // lane o < n_ops: the flag of operand o's partner wave (null: the operand does not apply here)
+  const gint* pflag = nullptr;
+  int pkind = -1;
+  if (lane < n_ops) {
+    const SpanOp& op = D.tab->ops[lane];
+    if (!(op.kind == 2 && (((h >> op.b) ^ (h >> op.b2)) & 1u))) {
+      pflag = (const gint*)D.flags + (int)(h ^ op.pmask) * kSpanWaves + wave;
+      pkind = op.kind;
+    }
+  }
 
   double2 prev[R];
 #pragma unroll
@@ -239,12 +260,6 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
         for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), u[bb][r]);
       }
     }
-    // ---- publish term k: u(w_{k-1}) of this term and raw w_{k-1} (stored at the end of k - 1) ----
-    if (u_mask || (need_raw && k > 1)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-
     // ---- phase 1: diagonal, register-bit drives and pairs ----
     double2 out[R];
 #pragma unroll
@@ -277,8 +292,16 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
     // ---- fused loop over the thread bits: the sweep's partner rows, then the thread pairs one at a
     // time, each next partner's rows in flight under the current one's FMAs ----
     const uint32_t itb = lds_byte(&S.it[0][0]);
+    // publish term k -- u(w_{k-1}) stored by the pre-pass, raw w_{k-1} at the end of term k - 1 --
+    // after J_PUB iterations, so the stores drain under the loop: per wave, s_waitcnt vmcnt(0)
+    // then one lane's flag store
+    const bool pub = u_mask || (need_raw && k > 1);
 #pragma unroll 1
     for (int j = 0; j < TB; ++j) {
+      if (j == J_PUB && pub) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       uint32_t ia;  // one VGPR base for the iteration row (broadcast reads)
       asm("v_mov_b32_e32 %0, %1" : "=v"(ia) : "s"(itb + (uint32_t)j * IW * 16u));
       const dv2 d0 = *(ldv2*)(size_t)ia, d1 = *(ldv2*)(size_t)(ia + 16u);
@@ -317,47 +340,80 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       }
     }
 
-    // ---- phase 4: cross-tile operands ----
-#pragma unroll 1
-    for (int o = 0; o < n_ops; ++o) {
-      const int kind = tab->ops[o].kind;
-      const int b = tab->ops[o].b;
-      if (kind == 2 && (((h >> b) ^ (h >> tab->ops[o].b2)) & 1u)) continue;  // pair absent here
-      const uint32_t p = h ^ tab->ops[o].pmask;
-      const bool raw = kind != 0;
-      if (!(raw && k == 1) && lane == 0) {
-        const gint* flag_pa = (const gint*)D.flags + (int)p * kSpanWaves + wave;
-        int spins = 0;
-        const int limit = 1 << 22;
-        while (__hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > limit ||
-              ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+    // ---- propagator-sum rows of this term, loaded now so their latency hides under phase 4 ----
+    bool upd[kMaxOut];
+    __amdgpu_buffer_rsrc_t accr[kMaxOut];
+    double2 av[kMaxOut][R];
+#pragma unroll
+    for (int j = 0; j < kMaxOut; ++j) {
+      upd[j] = j < n_out && coef_nterm(k, dj[j]) > 0;
+      accr[j] = (j == n_out - 1) ? acc_t
+                                 : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << P.n) + ((size_t)h << L), TBYTES);
+      if (upd[j] && k > 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) av[j][r] = bld(accr[j], voff, (uint32_t)(r * NT * 16));
+      }
+    }
+
+    // ---- phase 4: cross-tile operands.  Lane o of each wave polls operand o's partner flag, all
+    // at once (one round trip when the partners are ahead); then the operands' rows are loaded
+    // in batches of NB, every load of a batch in flight together ----
+    {
+      const bool need = pflag != nullptr && !(pkind != 0 && k == 1);
+      int spins = 0;
+      for (;;) {
+        const bool ok = !need || __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > g_span_spin_limit ||
+            ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          if (lane == 0) {
             S.fail = 1;
             atomicExch(err, 1);
-            break;
           }
+          break;
         }
       }
-      asm volatile("" ::: "memory");
-      const double2* sp = (raw && k == 1) ? P.buf[q ? 2 : 0] + ((size_t)p << L)
-                                          : slot_ptr(p, raw ? s : b, (k - 1) % kXSlots);
-      const __amdgpu_buffer_rsrc_t src = tile_rsrc(sp, TBYTES);
-      double2 uv[R];
+    }
+    asm volatile("" ::: "memory");  // the operand loads stay behind the poll
+#pragma unroll 1
+    for (int o0 = 0; o0 < n_ops; o0 += NB) {
+      double2 uv[NB][R];
+      bool app[NB];
 #pragma unroll
-      for (int r = 0; r < R; ++r) uv[r] = bld<kSc1>(src, voff, (uint32_t)(r * NT * 16));
-      if (kind == 0) {
+      for (int bb = 0; bb < NB; ++bb) {
+        const int o = o0 + bb;
+        app[bb] = false;
+        if (o >= n_ops) continue;
+        const int kind = tab->ops[o].kind;
+        app[bb] = !(kind == 2 && (((h >> tab->ops[o].b) ^ (h >> tab->ops[o].b2)) & 1u));
+        if (!app[bb]) continue;
+        const uint32_t p = h ^ tab->ops[o].pmask;
+        const bool raw = kind != 0;
+        const double2* sp = (raw && k == 1) ? P.buf[q ? 2 : 0] + ((size_t)p << L)
+                                            : slot_ptr(p, raw ? s : tab->ops[o].b, (k - 1) % kXSlots);
+        const __amdgpu_buffer_rsrc_t src = tile_rsrc(sp, TBYTES);
 #pragma unroll
-        for (int r = 0; r < R; ++r) out[r].x += uv[r].x, out[r].y += uv[r].y;
-      } else if (kind == 1) {
-        const int v = (int)((h >> b) & 1u);
-        const double cr = tab->ops[o].c[2 * v], ci = tab->ops[o].c[2 * v + 1];
+        for (int r = 0; r < R; ++r) uv[bb][r] = bld<kSc1>(src, voff, (uint32_t)(r * NT * 16));
+      }
 #pragma unroll
-        for (int r = 0; r < R; ++r) out[r] = smad<IMAG>(out[r], cr, ci, uv[r]);
-      } else {
-        const double g = tab->ops[o].c[0];
+      for (int bb = 0; bb < NB; ++bb) {
+        if (!app[bb]) continue;
+        const int o = o0 + bb;
+        const int kind = tab->ops[o].kind;
+        if (kind == 0) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) rfma(out[r], g, uv[r]);
+          for (int r = 0; r < R; ++r) out[r].x += uv[bb][r].x, out[r].y += uv[bb][r].y;
+        } else if (kind == 1) {
+          const int v = (int)((h >> tab->ops[o].b) & 1u);
+          const double cr = tab->ops[o].c[2 * v], ci = tab->ops[o].c[2 * v + 1];
+#pragma unroll
+          for (int r = 0; r < R; ++r) out[r] = smad<IMAG>(out[r], cr, ci, uv[bb][r]);
+        } else {
+          const double g = tab->ops[o].c[0];
+#pragma unroll
+          for (int r = 0; r < R; ++r) rfma(out[r], g, uv[bb][r]);
+        }
       }
     }
 
@@ -375,15 +431,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
     rows_lds<NT, R>(cur, tid, own);  // w_{k-1} (re-read: not held across the loop)
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
-      if (!(j < n_out && coef_nterm(k, dj[j]) > 0)) continue;
-      const __amdgpu_buffer_rsrc_t accj =
-          (j == n_out - 1) ? acc_t
-                           : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << P.n) + ((size_t)h << L), TBYTES);
-      double2 av[R];
-      if (k > 1) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) av[r] = bld(accj, voff, (uint32_t)(r * NT * 16));
-      }
+      if (!upd[j]) continue;
       const int nt = coef_nterm(k, dj[j]);
       const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);
       const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
@@ -392,10 +440,10 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         double2 a = make_double2(0.0, 0.0);
-        if (k > 1) a = cmad(av[r], c0.x, c0.y, prev[r]);
+        if (k > 1) a = cmad(av[j][r], c0.x, c0.y, prev[r]);
         a = cmad(a, c1.x, c1.y, own[r]);
         a = cmad(a, c2.x, c2.y, out[r]);
-        bst(accj, voff, (uint32_t)(r * NT * 16), a);
+        bst(accr[j], voff, (uint32_t)(r * NT * 16), a);
       }
     }
 #pragma unroll
@@ -417,7 +465,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
 
 }  // namespace
 
-#define DSE_SPAN_CONFIGS(X) X(12, 3) X(11, 2) X(11, 3) X(10, 2) X(10, 1)
+#define DSE_SPAN_CONFIGS(X) X(11, 2) X(10, 2) X(10, 1)
 
 bool span_supported(int L, int RB) {
 #define X(l, rb) if (L == l && RB == rb) return true;

@@ -3,9 +3,9 @@ CU, with per-term cross-tile hand-offs (u operands of the crossing pairs, raw ve
 crossing drives and the pairs between two tile-index bits).
 
 * The config-3 points (N = 14: center_off 13 qubits, center_on and shell_off 14) on k_span with
-  s = 2, 3 and 4 against the reference-H oracle traces (tests/golden/hpsi_traces_n14.npz, built
+  2^11- and 2^10-amplitude tiles (4 to 16 workgroups per register) against the reference-H oracle traces (tests/golden/hpsi_traces_n14.npz, built
   from the reference's own Hamiltonian) at 1e-10, as the production kernel is held
-  (test_gpu_config3.py).  shell_off at s >= 2 exercises every operand kind: u of crossing pairs,
+  (test_gpu_config3.py).  shell_off over >= 4 tiles exercises every operand kind: u of crossing pairs,
   and the raw partner of the pairs between two tile-index bits; center_on the raw partner under
   the rare spin's drive.
 * Bitwise repeatability of the spanned evolve in one context.
@@ -37,13 +37,17 @@ def _evolve(engine, probs, t, **opts):
         return engine.evolve(t)
     finally:
         engine.set_option("span", 0)
+        engine.set_option("span_tile", 0)
         engine.set_option("outputs_per_launch", 2)
         engine.set_option("matrix", 1)
         engine.clear()
 
 
-@pytest.mark.parametrize("s", [2, 3, 4])
-def test_spanned_registers_match_reference_n14(engine, golden, s):
+SPANS = [{"span_tile": 11}, {"span_tile": 10}, {"span": 3}]
+
+
+@pytest.mark.parametrize("opt", SPANS, ids=lambda o: "-".join(f"{k}{v}" for k, v in o.items()))
+def test_spanned_registers_match_reference_n14(engine, golden, opt):
     g = golden("hpsi_traces_n14.npz")
     t = g["t"]
     keys, probs = [], []
@@ -51,17 +55,17 @@ def test_spanned_registers_match_reference_n14(engine, golden, s):
         for delta in DELTAS:
             keys.append(f"{variant}_{delta}")
             probs.append(pb.build_problem(_params(variant, delta, t)))
-    obs, st = _evolve(engine, probs, t, span=s)
-    # every 14-qubit register spans (center_off's 13 qubits too where its tile fits k_span)
-    assert st["mode"] == 1 and st["span_problems"] >= 6, st
+    obs, st = _evolve(engine, probs, t, **opt)
+    # every register spans: 14 qubits over 8 / 16, 13 over 4 / 8 workgroups
+    assert st["mode"] == 1 and st["span_problems"] == 9, st
     worst = 0.0
     for i, key in enumerate(keys):
         for j, k in enumerate(OBS):
             err = float(np.max(np.abs(obs[i, j] - g[f"{key}_{k}"])))
             worst = max(worst, err)
-            assert err < 1e-10, (s, key, k, err)
+            assert err < 1e-10, (opt, key, k, err)
         np.testing.assert_allclose(obs[i, 6], g[f"{key}_state_norm"], rtol=0, atol=1e-12)
-    print(f"N=14 spanned over 2^{s} workgroups: max |GPU - reference-H oracle| = {worst:.2e}")
+    print(f"N=14 spanned ({opt}): max |GPU - reference-H oracle| = {worst:.2e}")
 
 
 @pytest.mark.parametrize("m", [2, 1])
@@ -70,7 +74,7 @@ def test_spanned_evolve_is_repeatable(engine, m):
     probs = [pb.build_problem(_params(v, d, t)) for v in VARIANTS for d in DELTAS]
     runs = []
     for _ in range(3):
-        obs, st = _evolve(engine, probs, t, span=3, outputs_per_launch=m)
+        obs, st = _evolve(engine, probs, t, span_tile=11, outputs_per_launch=m)
         assert st["span_problems"] == 9 and st["outputs_per_launch"] == m
         runs.append(obs)
     for r in runs[1:]:
@@ -78,16 +82,15 @@ def test_spanned_evolve_is_repeatable(engine, m):
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("s", [2, 3, 4])
-def test_lone_spanned_register_matches_default_kernel(engine, variant, s):
+@pytest.mark.parametrize("tile", [11, 10])
+def test_lone_spanned_register_matches_default_kernel(engine, variant, tile):
     """One register per evolve, 1 ms / 101 outputs (config 3's grid), 150 kHz (the stiffest
     point): k_span against the persistent interval kernel, both exact propagators (1e-11).  The
     13-qubit center_off register would take the propagator-matrix mode alone (matrix = 0 here)."""
     t = np.linspace(0.0, 1e-3, 101)
     p = pb.build_problem(_params(variant, 150e3, t))
     ref, st0 = _evolve(engine, [p], t, matrix=0)
-    obs, st = _evolve(engine, [p], t, span=s, matrix=0)
-    assert st0["span_problems"] == 0
-    assert st["span_problems"] == (1 if p.n_qubits - s >= 10 else 0), (p.n_qubits, s)
+    obs, st = _evolve(engine, [p], t, span_tile=tile, matrix=0)
+    assert st0["span_problems"] == 0 and st["span_problems"] == 1
     err = float(np.max(np.abs(obs - ref)))
     assert err < 1e-11, err

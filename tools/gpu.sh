@@ -64,7 +64,7 @@ for T in "$@"; do
       done
       cat $OUT/sytrd.jsonl ;;
     py)
-      s=${A[0]}; name=$(basename $s .py)
+      s=${A[0]}; name=$(basename $s .py)${A[1]:+_${A[1]}}
       timeout -k 10 ${PY_TIMEOUT:-600} python -u "${A[@]}" > $OUT/$name.out 2> $OUT/$name.err; rc=$?
       tail -c 1500 $OUT/$name.out; [ $rc -eq 0 ] || { tail -20 $OUT/$name.err; fail py $s; } ;;
     *) echo "unknown task $task"; exit 2 ;;

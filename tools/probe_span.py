@@ -2,10 +2,10 @@
 """Spanning-register timings (dse_span.hip): JSON lines of wall and kernel time.
 
     python3 tools/probe_span.py lone [reps]     one N = 14 register per evolve (center_on and
-                                                shell_off at 75 / 150 kHz), span 0 / 2 / 3 / 4
-    python3 tools/probe_span.py sweep [reps]    the bench's 192 evolutions with span 0 / 2 / 3 / 4
+                                                shell_off at 75 / 150 kHz), default / span_tile 11 / 10
+    python3 tools/probe_span.py sweep [reps]    the bench's 192 evolutions with default / span_tile 11 / 10
     python3 tools/probe_span.py shard [reps]    one GPU's share of the 64-point sweep on 8 GPUs
-                                                (8 points = 24 evolutions), span 0 / 2 / 3 / 4
+                                                (8 points = 24 evolutions), default / span_tile 11 / 10
 Grid: config 3's 1 ms / 101 outputs.  Kernel time = HIP events around every interval launch.
 """
 import json
@@ -24,9 +24,17 @@ from quantumsimulations_amd.sweep import VARIANTS, sweep_params, sweep_point_par
 T = np.linspace(0.0, 1e-3, 101)
 
 
+def setting(span):
+    """'0' default kernel, 'tL' option span_tile L, 'sS' option span S"""
+    if span in ("0", 0):
+        return {}
+    return {"span_tile" if span[0] == "t" else "span": int(span[1:])}
+
+
 def run(eng, probs, span, reps, label, **opts):
     eng.clear()
-    eng.set_option("span", span)
+    for k, v in setting(span).items():
+        eng.set_option(k, v)
     for k, v in opts.items():
         eng.set_option(k, v)
     for p in probs:
@@ -39,6 +47,7 @@ def run(eng, probs, span, reps, label, **opts):
         walls.append((time.perf_counter() - t0) * 1e3)
         kms.append(st["step_kernel_ms"])
     eng.set_option("span", 0)
+    eng.set_option("span_tile", 0)
     eng.clear()
     terms = st["h_applications"]
     rec = {"case": label, "span": span, "n_probs": len(probs), "wall_ms": min(walls),
@@ -55,7 +64,7 @@ def run(eng, probs, span, reps, label, **opts):
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "lone"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    spans = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 2, 3, 4]
+    spans = sys.argv[3].split("/") if len(sys.argv) > 3 else ["0", "t11", "t10"]
     with Engine(0) as eng:
         if what == "lone":
             for variant in ("center_on", "shell_off"):
