@@ -9,9 +9,10 @@ resident in HBM); each timed step resets every state to psi0 and runs the whole
 evolution (Chebyshev interval kernels + observable reductions) to t_final.
 
 value = detuning-points / hour over the whole job (points of all ranks / max rank time).
-Multi-GPU (torchrun, one process per GPU): weak scaling; rank r of N takes the
-detunings j = r (mod N) of linspace(0, 150 kHz, 64 N), i.e. 64 distinct points per
-rank, no data-path collective (evolutions are independent).
+Multi-GPU (torchrun, one process per GPU), no data-path collective (evolutions are independent):
+  --scaling strong (default; BASELINE config 3 as stated: ONE 64-point sweep over the N GPUs):
+      rank r of N takes the detunings j = r (mod N) of linspace(0, 150 kHz, 64) -- 64/N points each;
+  --scaling weak: rank r takes j = r (mod N) of linspace(0, 150 kHz, 64 N) -- 64 points per rank.
 
 Extra fields of the JSON line:
   roofline       the dominant kernel (k_interval, HIP events around every launch on its own
@@ -33,6 +34,9 @@ Extra fields of the JSON line:
                  3 variants, 30 s / 20 000 outputs) timed whole on the dense eigen-propagator
   large_register rank 0, N = 1 only: config 5 on one GPU (N = 30, Walsh-Hadamard engine) against
                  the HBM roofline, with exact-invariant checks (norm, energy); --no-large skips it
+  strong_shard_8gpu  rank 0, N = 1 only: the 8-GPU strong split predicted on one GPU -- each of
+                 the 8 ranks' shards (8 points = 24 evolutions) timed alone on this GPU; the
+                 heaviest shard's wall time is the 8-GPU step time (ms/ODE-step beside it)
   partitioned    N = 2, 4, 8 only, after the timed sweep: config 5 with the N = 30 register split
                  over the N ranks (tools/bench_partitioned.py as a child process per rank, RCCL
                  index-swap all-to-all over xGMI): ms per H application, exchanged bytes per rank,
@@ -83,6 +87,9 @@ def parse():
                     help="persistent mode: observables on a second stream per lane (1)")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
     ap.add_argument("--n-det", type=int, default=N_DET)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default=os.environ.get("DSE_BENCH_SCALING", "strong"),
+                    help="strong: one n-det sweep split over the ranks (BASELINE config 3); weak: n-det per rank")
+    ap.add_argument("--no-shard8", action="store_true", help="skip the 8-GPU strong-split prediction leg")
     ap.add_argument("--no-large", action="store_true", help="skip the config-5 single-GPU leg")
     ap.add_argument("--no-full", action="store_true", help="skip the reference-grid (30 s) leg")
     ap.add_argument("--full-intervals", type=int, default=16,
@@ -388,9 +395,49 @@ def reference_default_leg(device: int, k_cheb: int = 20):
     }
 
 
-def shard_detunings(n_det_per_rank: int, rank: int, world: int) -> np.ndarray:
-    """Weak scaling: rank r takes detunings j = r (mod world) of linspace(0, 150 kHz, n*world)."""
-    return np.linspace(0.0, DELTA_MAX, n_det_per_rank * world)[rank::world]
+def shard_detunings(n_det: int, rank: int, world: int, scaling: str = "strong") -> np.ndarray:
+    """strong: rank r takes detunings j = r (mod world) of linspace(0, 150 kHz, n_det) (one sweep
+    split over the ranks); weak: j = r (mod world) of linspace(0, 150 kHz, n_det * world)."""
+    total = n_det if scaling == "strong" else n_det * world
+    return np.linspace(0.0, DELTA_MAX, total)[rank::world]
+
+
+def strong_shard_leg(eng, n_sea: int, n_det: int, world_pred: int = 8, reps: int = 3) -> dict:
+    """The world_pred-GPU strong split of the n_det-point sweep, predicted on this GPU: every rank's
+    shard (n_det / world_pred points x 3 variants) evolved alone in this context, reps times
+    (minimum kept); the step time of the split is the heaviest shard's.  One GPU per shard, no
+    collective: the prediction omits only the ranks' barrier."""
+    import torch
+
+    from quantumsimulations_amd import problem as pb
+    from quantumsimulations_amd.sweep import sweep_params
+    t = np.linspace(0.0, T_FINAL, STEPS_T)
+    shards = []
+    for r in range(world_pred):
+        dets = shard_detunings(n_det, r, world_pred, "strong")
+        eng.clear()
+        for p in sweep_params(n_sea, dets, T_FINAL, STEPS_T):
+            eng.add(pb.build_problem(p))
+        eng.evolve(t)  # warm-up
+        walls = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, st = eng.evolve(t)
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) * 1e3)
+        ode = st["h_applications"] / (3 * len(dets))
+        shards.append({"rank": r, "points": len(dets), "wall_ms": min(walls), "kernel_ms": st["step_kernel_ms"],
+                       "span_problems": st["span_problems"], "max_degree": st["max_degree"],
+                       "ms_per_ode_step": min(walls) / ode})
+    eng.clear()
+    worst = max(shards, key=lambda x: x["wall_ms"])
+    return {"gpus": world_pred, "points": n_det, "step_ms": worst["wall_ms"],
+            "value": n_det / (worst["wall_ms"] * 1e-3) * 3600.0, "unit": "detuning-points/hour",
+            "ms_per_ode_step": worst["ms_per_ode_step"], "heaviest_rank": worst["rank"],
+            "shards": shards,
+            "note": (f"each of the {world_pred} ranks' shards of the {n_det}-point sweep timed alone on this GPU "
+                     "(min of reps); the split's step time is the heaviest shard's")}
 
 
 def timed_steps(step, steps: int, warmup: int, sync, dist=None) -> float:
@@ -496,7 +543,7 @@ def main():
     from quantumsimulations_amd.engine import Engine
     from quantumsimulations_amd.sweep import sweep_params
 
-    my_det = shard_detunings(args.n_det, rank, world)
+    my_det = shard_detunings(args.n_det, rank, world, args.scaling)
     params = sweep_params(args.n_sea, my_det, T_FINAL, STEPS_T)
     probs = [pb.build_problem(p) for p in params]
     t = np.linspace(0.0, T_FINAL, STEPS_T)
@@ -527,7 +574,7 @@ def main():
 
     if world > 1:
         note(f"rank {rank}: timed steps done ({dt:.3f} s)")
-    points = len(my_det) * world * args.steps
+    points = (args.n_det if args.scaling == "strong" else len(my_det) * world) * args.steps
     value = points / dt * 3600.0
     h_apps = sum(s["h_applications"] for s in stats)
     mode = stats[-1]["mode"]
@@ -614,15 +661,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64 (complex128 state)",
         "data": "synthetic (reference physical constants, deterministic; no external data)",
         "config": {
-            "workload": (f"config 3: n_sea={args.n_sea}+1 rare (N=14 qubits), {len(my_det)} detunings in "
-                         f"[0,150 kHz] x 3 variants = {3 * len(my_det)} evolutions per GPU, "
-                         f"t_final={T_FINAL}s, {STEPS_T} outputs, 7 observables"),
-            "global_points_per_step": len(my_det) * world,
+            "workload": (f"config 3: n_sea={args.n_sea}+1 rare (N=14 qubits), "
+                         + (f"one {args.n_det}-point sweep split over {world} GPU(s)" if args.scaling == "strong"
+                            else f"{args.n_det} points per GPU") +
+                         f" ({len(my_det)} detunings in [0,150 kHz] x 3 variants = {3 * len(my_det)} evolutions"
+                         f" on rank 0), t_final={T_FINAL}s, {STEPS_T} outputs, 7 observables"),
+            "global_points_per_step": args.n_det if args.scaling == "strong" else len(my_det) * world,
             "evolutions_per_step_per_gpu": len(probs),
             "propagator": "exact Chebyshev (tol 1e-14)",
             "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(mode, "streaming"),
@@ -631,18 +680,24 @@ def main():
             "outputs_per_launch": stats[-1].get("outputs_per_launch"),
             "ms_per_ode_step": (dt / args.steps) / (h_apps / args.steps / len(probs)) * 1e3,
             "h_applications_per_step": h_apps / args.steps,
-            "parallelism": f"evolution-sharded x{world} (no collectives)",
+            "parallelism": f"evolution-sharded x{world} ({args.scaling} scaling, no collectives)",
+            "span_problems": stats[-1].get("span_problems"),
         },
         "roofline": roof,
     }
     if not args.no_full:
         try:
-            line["full_sweep"] = full_sweep(eng, probs, len(my_det) * world, args.full_intervals,
+            line["full_sweep"] = full_sweep(eng, probs, args.n_det if args.scaling == "strong" else len(my_det) * world, args.full_intervals,
                                             args.full_repeats, torch.cuda.synchronize, dist)
         except Exception as exc:  # report, never hide
             line["full_sweep"] = {"error": repr(exc)}
     if cpu is not None:
         line["cpu_baseline"] = cpu
+    if rank == 0 and world == 1 and not args.no_shard8:
+        try:
+            line["strong_shard_8gpu"] = strong_shard_leg(eng, args.n_sea, args.n_det)
+        except Exception as exc:  # report, never hide
+            line["strong_shard_8gpu"] = {"error": repr(exc)}
     eng.close()
     if rank == 0 and world == 1 and not args.no_config2:
         try:

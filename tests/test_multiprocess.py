@@ -21,12 +21,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, scaling, out):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    det = bench.shard_detunings(4, rank, world)
+    det = bench.shard_detunings(4, rank, world, scaling)
     n_calls = [0]
 
     def step():
@@ -76,16 +76,19 @@ def test_bench_partitioned_leg_plumbing_gloo(case):
             assert "boom" in rep0["stderr_tail"]
 
 
-def test_bench_sharding_and_timing_gloo():
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_sharding_and_timing_gloo(scaling):
+    """strong (default, BASELINE config 3): one 4-point sweep split over the 2 ranks; weak: 4
+    points per rank.  Either way the shards are disjoint and cover the global grid."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), scaling, out), nprocs=world, join=True)
     dets = [out[r][0] for r in range(world)]
-    # disjoint shards covering the global grid of 4 * world detunings
+    total = 4 if scaling == "strong" else 4 * world
     allv = sorted(dets[0] + dets[1])
-    np.testing.assert_array_equal(allv, np.linspace(0.0, bench.DELTA_MAX, 4 * world))
-    assert len(dets[0]) == len(dets[1]) == 4
+    np.testing.assert_array_equal(allv, np.linspace(0.0, bench.DELTA_MAX, total))
+    assert len(dets[0]) == len(dets[1]) == total // world
     # every rank reports the same (maximum) time, at least the slow rank's 3 x 40 ms
     assert out[0][1] == out[1][1] and out[0][1] >= 0.12
     assert out[0][2] == out[1][2] == 4          # 1 warmup + 3 timed
@@ -266,3 +269,12 @@ def test_write_sweep_png_workers_match_serial_report(tmp_path):
     assert tree(tmp_path / "w1") == tree(tmp_path / "w3")
     assert len([f for f in tree(tmp_path / "w3") if f.endswith(".png")]) >= 2 * 8
     assert pages[1] == pages[3] > 8
+
+
+def test_strong_split_of_the_64_point_sweep_over_8_gpus():
+    """BASELINE config 3 on 8 GPUs: each rank 8 of the 64 detunings, interleaved (j = r mod 8),
+    disjoint, covering linspace(0, 150 kHz, 64); the last rank holds the stiffest point (150 kHz)."""
+    shards = [bench.shard_detunings(64, r, 8, "strong") for r in range(8)]
+    assert all(len(x) == 8 for x in shards)
+    np.testing.assert_array_equal(np.sort(np.concatenate(shards)), np.linspace(0.0, bench.DELTA_MAX, 64))
+    assert shards[7][-1] == bench.DELTA_MAX
