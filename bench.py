@@ -152,7 +152,9 @@ def cpu_baseline(fraction: float, cores: int):
     return json.loads(res.stdout.strip().splitlines()[-1])
 
 
-WHT_PMC_N30 = os.path.join(ROOT, "profiles", "r01", "wht_n30_pmc_traffic.json")
+WHT_PMC_N30 = next((q for q in (os.path.join(ROOT, "profiles", r, "wht_n30_pmc_traffic.json")
+                                 for r in ("r04", "r01")) if os.path.exists(q)),
+                   os.path.join(ROOT, "profiles", "r01", "wht_n30_pmc_traffic.json"))
 
 
 def diag_energy(prob) -> float:
@@ -190,6 +192,9 @@ def large_register(device: int, n_sea: int = 29):
     e0 = diag_energy(prob)
     per_term_ms = st["step_kernel_ms"] / max(st["timed_launches"], 1)
     gbs = bpa * (1 << n) / (per_term_ms * 1e-3) / 1e9
+    s8d = 80.0 * (1 << n) / (per_term_ms * 1e-3) / 1e9
+    fpa = flops_per_amp(prob)
+    fl = fpa * (1 << n)
     traffic = None  # HBM-side bytes per H application (MODE_GEN passes) from the counter passes
     try:
         with open(WHT_PMC_N30) as f:
@@ -208,9 +213,19 @@ def large_register(device: int, n_sea: int = 29):
         "h_applications": st["h_applications"],
         "kernel_ms_per_h_application": per_term_ms,
         "wall_ms_per_h_application_incl_setup": wall / st["h_applications"] * 1e3,
-        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa, "traffic": traffic,
-                     "traffic_source": os.path.relpath(WHT_PMC_N30, ROOT)},
+        # SURVEY.md §8(d)'s pricing of a fused Chebyshev term (80 B/amp: the bytes a one-pass
+        # streaming term would move) and the FP64 rate of the algorithmic flops: at N = 30 the
+        # arithmetic intensity 1072 flop / 80 B = 13.4 is past the FP64 ridge (78.6 / 8 = 9.8), so
+        # FP64 is §8(d)'s binding bound; the pass-traffic figure prices the engine's own passes
+        "roofline": {"bound": "fp64", "achieved": fl / (per_term_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": fl / (per_term_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                     "flops_per_amp_per_h": fpa,
+                     "s8d_hbm": {"achieved": s8d, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": s8d / HBM_PEAK_GBS,
+                                 "bytes_per_amp_per_h": 80.0},
+                     "passes_hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa},
+                     "traffic": traffic, "traffic_per_amp": traffic / (1 << n) if traffic else None,
+                     "traffic_source": os.path.relpath(WHT_PMC_N30, ROOT) if traffic else None},
         "check": check,
     }
 

@@ -98,6 +98,21 @@ __device__ __forceinline__ ddv dd_div(ddv a, ddv b) {
   return dd_fast(q1, q2);
 }
 
+// The diagonal element <x|H'|x> EXACTLY (to double-double): every term field_i s_i, zz_ij s_i s_j is
+// an fp64 coefficient times +-1/2 or +-1/4 (exact), so only the sum rounds -- k_dense_h's fp64
+// diagonal carries a few ulp of it (~|H| 1e-16), which at the reference grid's 30 s would be a
+// phase of ~1e-8.  The refined eigenvalues are therefore those of H' with the exact diagonal.
+__device__ __forceinline__ ddv dense_diag_dd(const DenseProb& P, uint32_t x) {
+  const int n = P.n;
+  ddv d = {0.0, 0.0};
+  for (int i = 0; i < n; ++i) {
+    const double si = 0.5 - (double)((x >> i) & 1u);
+    d = dd_add(d, ddv{P.field[i] * si, 0.0});
+    for (int j = i + 1; j < n; ++j) d = dd_add(d, ddv{P.zz[i * n + j] * (si * (0.5 - (double)((x >> j) & 1u))), 0.0});
+  }
+  return d;
+}
+
 // Rayleigh quotient of eigenvector a (column a of V) in double-double: one workgroup per
 // (eigenvector, problem); thread partials summed in a fixed order (deterministic)
 __global__ void __launch_bounds__(256)
@@ -109,7 +124,7 @@ k_dense_rq(const DenseProb* __restrict__ probs, int dim) {
   ddv num = {0.0, 0.0}, den = {0.0, 0.0};
   for (uint32_t x = threadIdx.x; x < (uint32_t)dim; x += 256u) {
     const double vx = v[x];
-    ddv y = dd_prod(dense_diag(P, x), vx);
+    ddv y = dd_mul_d(dense_diag_dd(P, x), vx);
     dense_offdiag(P, x, [&](uint32_t yy, double c) { y = dd_add(y, dd_prod(c, v[yy])); });
     num = dd_add(num, dd_mul_d(y, vx));
     den = dd_add(den, dd_prod(vx, vx));

@@ -152,6 +152,7 @@ hipError_t launch_span(int L, int RB, bool imag, const DevProb* probs, const Spa
                        hipStream_t st);
 bool span_supported(int L, int RB);
 hipError_t set_span_spin_limit(int limit);
+hipError_t set_span_ablate(int mask);
 hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu);
 
 // Coefficient row of output j of offset set `set`: kcap1 + 1 entries, row[0].x = the degree d of

@@ -1372,6 +1372,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "ablate") {  // diagnostics only: skip kernel sections (results become wrong)
     HIPC(set_ablate((int)value));
     HIPC(set_ablate_interval((int)value));
+  } else if (k == "span_ablate") {  // diagnostics only: skip k_span sections (results become wrong)
+    HIPC(set_span_ablate((int)value));
   } else if (k == "probe_items") {  // diagnostics only: dse_time_step_kernel launches this many items
     ctx->probe_items = (int64_t)value;
   } else if (k == "max_degree") {

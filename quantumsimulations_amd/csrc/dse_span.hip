@@ -38,6 +38,13 @@ namespace dse {
 // Polls of the partners' flags before a hand-off is declared failed (s_sleep 1 between polls);
 // negative: fail at once (diagnostics: exercises the fallback)
 __device__ int g_span_spin_limit = 1 << 22;
+// Diagnostic ablation mask (0 in production; results are wrong otherwise): 1 no pre-pass, 2 no
+// publish, 4 no poll, 8 no operand loads, 16 no propagator sums, 32 no fused loop, 64 no raw store
+__device__ int g_span_ablate = 0;
+
+hipError_t set_span_ablate(int mask) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_span_ablate), &mask, sizeof(int));
+}
 
 hipError_t set_span_spin_limit(int limit) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_span_spin_limit), &limit, sizeof(int));
@@ -132,7 +139,8 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
   const __amdgpu_buffer_rsrc_t psi_me = tile_rsrc(P.buf[q ? 2 : 0] + ((size_t)h << L), TBYTES);
   const __amdgpu_buffer_rsrc_t acc_t = tile_rsrc(P.buf[q ? 0 : 2] + ((size_t)h << L), TBYTES);
   gint* const flag_me = (gint*)D.flags + (int)h * kSpanWaves + wave;
-  const int u_mask = tab->u_mask, n_ops = tab->n_ops;
+  const int ab = g_span_ablate;
+  const int u_mask = (ab & 1) ? 0 : tab->u_mask, n_ops = (ab & 8) ? 0 : tab->n_ops;
   const bool need_raw = tab->need_raw != 0;
 
   const double* crow = (const double*)coef_row(P, set, 0);
@@ -297,8 +305,8 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
     // then one lane's flag store
     const bool pub = u_mask || (need_raw && k > 1);
 #pragma unroll 1
-    for (int j = 0; j < TB; ++j) {
-      if (j == J_PUB && pub) {
+    for (int j = 0; j < ((ab & 32) ? 0 : TB); ++j) {
+      if (j == J_PUB && pub && !(ab & 2)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -340,6 +348,10 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       }
     }
 
+    if ((ab & 32) && pub && !(ab & 2)) {  // diagnostics: no loop, publish here
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // ---- propagator-sum rows of this term, loaded now so their latency hides under phase 4 ----
     bool upd[kMaxOut];
     __amdgpu_buffer_rsrc_t accr[kMaxOut];
@@ -349,6 +361,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       upd[j] = j < n_out && coef_nterm(k, dj[j]) > 0;
       accr[j] = (j == n_out - 1) ? acc_t
                                  : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << P.n) + ((size_t)h << L), TBYTES);
+      if (ab & 16) upd[j] = false;
       if (upd[j] && k > 1) {
 #pragma unroll
         for (int r = 0; r < R; ++r) av[j][r] = bld(accr[j], voff, (uint32_t)(r * NT * 16));
@@ -359,7 +372,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
     // at once (one round trip when the partners are ahead); then the operands' rows are loaded
     // in batches of NB, every load of a batch in flight together ----
     {
-      const bool need = pflag != nullptr && !(pkind != 0 && k == 1);
+      const bool need = pflag != nullptr && !(pkind != 0 && k == 1) && !(ab & 4);
       int spins = 0;
       for (;;) {
         const bool ok = !need || __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k;
@@ -453,7 +466,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       d.x = out[r].x, d.y = out[r].y;
       *(sdv2*)(size_t)(nxt + ((uint32_t)(r * NT + tid)) * 16u) = d;
     }
-    if (need_raw && k < K) {  // w_k for the partners' term k + 1
+    if (need_raw && k < K && !(ab & 64)) {  // w_k for the partners' term k + 1
       const __amdgpu_buffer_rsrc_t dst = tile_rsrc(slot_ptr(h, s, k % kXSlots), TBYTES);
 #pragma unroll
       for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), out[r]);

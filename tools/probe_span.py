@@ -78,6 +78,12 @@ def main():
                         else:
                             print(json.dumps({"check": f"{variant}_{int(d / 1e3)}k", "span": s,
                                               "max_abs_diff_vs_span0": float(np.max(np.abs(obs - ref)))}), flush=True)
+        elif what == "ablate":  # probe_span.py ablate <reps> <setting> <mask/mask/...>: k_span sections off
+            p = pb.build_problem(sweep_point_params(13, 150e3, "center_on", T[-1], len(T)))
+            masks = [int(m) for m in (sys.argv[4].split("/") if len(sys.argv) > 4 else ["0"])]
+            for m in masks:
+                run(eng, [p], spans[0], reps, f"center_on_150k_ablate{m}", span_ablate=m)
+            eng.set_option("span_ablate", 0)
         else:
             n_pts = 64 if what == "sweep" else 8
             dets = np.linspace(0.0, 150e3, 64)
