@@ -118,7 +118,7 @@ struct DevProb {
 // CUs.  In a tile, thread t of NT = 2^(L - RB) owns the R = 2^RB amplitudes x = r * NT + t.
 constexpr int kSpanMaxTop = 4;   // top (tile-index) bits: up to 16 workgroups per register
 constexpr int kSpanWaves = 16;   // hand-off flags per tile: one per wave (<= 1024 threads)
-constexpr int kSpanMaxIt = 160;  // fused-loop iteration rows (dv2): TB x (4 + pairs per iteration)
+constexpr int kSpanMaxIt = 160;  // fused-loop coefficient rows (dv2): TB x (8 + pairs per iteration) / 2
 constexpr int kSpanMaxOps = kSpanMaxTop + kSpanMaxTop * (kSpanMaxTop - 1) / 2;
 // One cross-tile operand of every tile's H application (phase 4 of k_span):
 //   kind 0  u_b of the partner h ^ e_b (its slot b): flip_b w + sum_j g_jb [x_j == h_b] w(x ^ e_j)
@@ -137,8 +137,9 @@ struct alignas(16) SpanTab {
   SpanOp ops[kSpanMaxOps];
   int rflip_mask, u_mask, n_ops, need_raw;  // need_raw: some operand reads a partner's raw w
   int n_it, pad[3];
-  // iteration j (thread bit j): [0] re0 im0, [1] re1 im1 (drive of j by output value t_j),
-  // [2] [3] pairs (j, register bit 0..3), [4 + q] thread pair q of the iteration (mask bits, g)
+  // coefficient row of iteration j (thread bit j), as doubles: c0i c1i c0r c1r (drive of j by the
+  // output value t_j), g of the pairs (j, register bit 0..3), then g of the iteration's thread pairs
+  // in the canonical schedule (dse_span.hip span_pair_mask)
   double2 it[kSpanMaxIt];
 };
 struct SpanDesc {

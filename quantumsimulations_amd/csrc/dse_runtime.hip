@@ -162,6 +162,7 @@ struct dse_ctx {
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
   int handoff_fallbacks = 0;        // this evolve call re-ran on the streaming kernels after a hand-off timeout (0/1)
+  bool rerun = false;               // that re-run: the dense engine's results of the first pass are kept
   int* d_err_cur = nullptr;         // the hand-off error word of the running persistent evolve (else null)
   double* d_allreduce = nullptr;    // RCCL all-reduce staging buffer of the observable sums (grow-only)
   size_t allreduce_cap = 0;         // in doubles
@@ -2176,6 +2177,16 @@ bool matrix_eligible(const HostProblem& P, const double* t, int n_t, double* dt_
 // workgroups per CU (one at 2^13, LDS), products over the half matrix at ~5 TB/s plus ~5 us for the
 // reduction launch; complex build (k_interval column mode): as the chain's terms, two workgroups
 // per CU below 2^13, products over the whole matrix (zgemv) at ~3 TB/s.
+// device bytes of matrix_run for register P on n_t outputs (U's stored tiles or columns, the
+// states, the products' partials; the small tables are within the rounding)
+double matrix_bytes(const HostProblem& P, int n_t) {
+  const double dim = std::ldexp(1.0, P.n_local);
+  const double nb = dim / kSymvBlock;
+  const bool real = dense_eligible(P) && ucols_supported(P.L) && P.n_local == P.L;
+  const double u = real ? nb * (nb + 1) / 2 * kSymvBlock * kSymvBlock : dim * dim;
+  return 16.0 * (u + dim * n_t + (real ? nb * dim : 0.0)) + (1 << 20);
+}
+
 bool matrix_cheaper(const HostProblem& P, double dt, int n_t, int n_cu) {
   const double dim = std::ldexp(1.0, P.n_local);
   const double alpha = 0.5 * (P.e_max - P.e_min);
@@ -2441,21 +2452,25 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
   const int n = P.n;
   const int TB = L - RB;
   const int npi = (TB * (TB - 1) / 2 + TB - 1) / TB;
-  const int iw = 4 + npi;
+  const int iw = (8 + npi + 1) / 2;  // dv2 per coefficient row (dse_span.hip SpanGeo::IW)
   if (TB * iw > kSpanMaxIt || L > 16 || RB > 4 || s > kSpanMaxTop || n != L + s) return DSE_ERR_ARG;
   std::memset(&T, 0, sizeof(T));
   T.n_it = TB * iw;
-  auto it = [&](int j, int e) -> double2& { return T.it[j * iw + e]; };
-  std::vector<std::pair<uint32_t, double>> tpairs;
+  // row j as doubles: c0i c1i c0r c1r (drive of thread bit j by output value), g with register
+  // bits 0..3, then the thread pairs of iteration j in the canonical schedule (span_pair_mask)
+  auto row = [&](int j, int e) -> double& {
+    double2& d = T.it[j * iw + e / 2];
+    return (e & 1) ? d.y : d.x;
+  };
   for (int i = 0; i < n; ++i)
     for (int j = i + 1; j < n; ++j) {
       const double g = P.pair[i * n + j];
       if (g == 0.0) continue;
-      if (j < TB) {
-        tpairs.push_back({(1u << i) | (1u << j), g});
+      if (j < TB) {  // canonical index of (i, j): lexicographic over a < b < TB
+        const int p = i * TB - i * (i + 1) / 2 + (j - i - 1);
+        row(p / npi, 8 + p % npi) = g;
       } else if (j < L && i < TB) {
-        const int r = j - TB;
-        (r & 1 ? it(i, 2 + r / 2).y : it(i, 2 + r / 2).x) = g;
+        row(i, 4 + (j - TB)) = g;
       } else if (j < L) {
         T.rr_g[rr_index(i - TB, j - TB)] = g;
       } else if (i < L) {
@@ -2471,12 +2486,6 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
         T.need_raw = 1;
       }
     }
-  if ((int)tpairs.size() > TB * npi) return DSE_ERR_ARG;
-  for (size_t p = 0; p < tpairs.size(); ++p) {
-    double2& e = it((int)(p / npi), 4 + (int)(p % npi));
-    e.x = __builtin_bit_cast(double, (uint64_t)tpairs[p].first);
-    e.y = tpairs[p].second;
-  }
   for (int b = 0; b < n; ++b) {
     double f[4];
     for (int c = 0; c < 4; c += 2) {  // as build_tables: cos(pi/2) residues dropped
@@ -2486,8 +2495,10 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
     }
     if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
     if (b < TB) {
-      it(b, 0) = make_double2(f[0], f[1]);
-      it(b, 1) = make_double2(f[2], f[3]);
+      row(b, 0) = f[1];
+      row(b, 1) = f[3];
+      row(b, 2) = f[0];
+      row(b, 3) = f[2];
     } else if (b < L) {
       for (int c = 0; c < 4; ++c) T.rflip[b - TB][c] = f[c];
       T.rflip_mask |= 1 << (b - TB);
@@ -2568,7 +2579,12 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       if (!ctx->probs[pi].side()) ++n_cheb, last = (int)pi;
     if (n_cheb == 1 && ctx->matrix && ctx->persistent) {
       HostProblem& P = ctx->probs[last];
-      if (matrix_eligible(P, t, n_t, &matrix_dt) &&
+      // the matrix-mode buffers must fit 80% of the free memory (plus what the context already
+      // holds for them); otherwise the register stays on the per-interval kernels
+      size_t free_b = 0, total_b = 0;
+      HIPC(hipMemGetInfo(&free_b, &total_b));
+      const bool fits = matrix_bytes(P, n_t) <= 0.8 * (double)free_b + (double)ctx->mx_cap;
+      if (fits && matrix_eligible(P, t, n_t, &matrix_dt) &&
           (ctx->matrix == 2 || matrix_cheaper(P, matrix_dt, n_t, ctx->n_cu))) {
         P.mx = true;
         matrix_pi = last;
@@ -3083,7 +3099,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   if (any_small && (rc = small_launch(ctx, t, n_t, tol, &small_happl, &small_launches))) return rc;
 
   double dense_ms = 0.0, dense_eig_ms = 0.0;
-  if (any_dense && (rc = dense_run(ctx, t, n_t, obs_out, &dense_ms, &dense_eig_ms))) return rc;
+  // (the re-run after a hand-off timeout keeps the first pass's dense results: dense_run completed
+  // and wrote them before any interval launch, and its register choice depends only on t)
+  if (any_dense && !ctx->rerun && (rc = dense_run(ctx, t, n_t, obs_out, &dense_ms, &dense_eig_ms))) return rc;
   double matrix_happl = 0.0;
   if (matrix_pi >= 0 && (rc = matrix_run(ctx, matrix_pi, t, n_t, matrix_dt, tol, obs_out, &matrix_happl))) return rc;
   phase("psi0/small");
@@ -3361,7 +3379,9 @@ int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_o
   HIPC(hipMemcpy(d_err, &zero, sizeof(int), hipMemcpyHostToDevice));
   const int saved = ctx->persistent;
   ctx->persistent = 0;
+  ctx->rerun = true;
   rc = evolve_impl(ctx, t, n_t, tol, obs_out, stats);
+  ctx->rerun = false;
   ctx->persistent = saved;
   ctx->d_err_cur = nullptr;
   ctx->handoff_fallbacks = 1;

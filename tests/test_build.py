@@ -70,3 +70,16 @@ def test_wht_passes_do_not_spill(tmp_path):
     passes += persistent
     assert all(sp == 0 for _, sp, _ in kernels), kernels
     assert all(sc == 0 for _, _, sc in passes), passes
+
+
+def test_span_kernel_does_not_spill(tmp_path):
+    """k_span (dse_span.hip) keeps out, w_{k-2} and the pipelined partner rows in registers at two
+    waves per SIMD for the 512-thread configurations (2^11 tiles x 4 rows, 2^10 x 2 rows)."""
+    res = subprocess.run(
+        [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-c",
+         os.path.join(CSRC, "dse_span.hip"), "-o", str(tmp_path / "span.o"), "-Rpass-analysis=kernel-resource-usage"],
+        capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr[-2000:]
+    kernels = [k for k in _resources(res.stderr) if "k_span" in k[0]]
+    assert len(kernels) >= 4, kernels
+    assert all(sp == 0 and sc == 0 for _, sp, sc in kernels), kernels
