@@ -319,6 +319,24 @@ def full_sweep_dense(device: int, dets, sync, dist=None):
     }
 
 
+def matrix_kernels(st) -> dict:
+    """Propagator-matrix mode's device time (HIP events in libdse): the column build of U (k_ucols)
+    and the n_t - 2 products psi_{j+1} = U psi_j (k_symv + k_symv_reduce).  A product reads U's
+    stored 64 x 64 tiles on and above the diagonal once (complex symmetric U: 130 MiB at N = 12, held
+    in the 256 MiB Infinity Cache between products) plus x; priced against the HBM peak, which the
+    MALL-resident stream may exceed."""
+    if st.get("mode") != 5 or not st.get("matrix_products"):
+        return {"used": False}
+    per = st["matrix_products_ms"] / st["matrix_products"]
+    gbs = st["matrix_bytes_per_product"] / (per * 1e-3) / 1e9
+    return {"used": True, "build_ms": st["matrix_build_ms"], "products": st["matrix_products"],
+            "products_ms": st["matrix_products_ms"], "us_per_product": per * 1e3,
+            "roofline": {"kernel": "k_symv + k_symv_reduce (half-matrix symmetric product)", "bound": "hbm",
+                         "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "bytes_per_product": st["matrix_bytes_per_product"],
+                         "note": "U's stored tiles are Infinity-Cache resident across the products"}}
+
+
 def config2_leg(device: int):
     """BASELINE config 2 through the drop-in surface: one N = 12 center_on evolution (n_sea = 11,
     50 kHz, 2 ms / 201 outputs) by simulate_rare (dipolar_ensemble_with_rare.py:611 replaced), wall
@@ -362,7 +380,9 @@ def config2_leg(device: int):
         "max_abs_err_vs_exact": err, "tolerance": 1e-8,
         "engine": {"mode": st["mode"], "max_degree": st["max_degree"],
                    "h_applications": st["h_applications"], "launches": st["step_launches"],
-                   "kernel_ms": st["step_kernel_ms"], "dense_problems": st["dense_problems"]},
+                   "kernel_ms": st["step_kernel_ms"], "dense_problems": st["dense_problems"],
+                   "span_problems": st["span_problems"]},
+        "matrix_mode": matrix_kernels(st),
         "ms_per_h_application": float(np.median(walls)) / max(st["h_applications"], 1),
         "unmodified_caller_n14": {"calls": 3, "grid": "1 ms / 101 outputs, 75 kHz",
                                   "wall_ms": serial14, "ms_per_call": serial14 / 3},

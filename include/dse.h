@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 9
+#define DSE_ABI_VERSION 10
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -107,6 +107,10 @@ typedef struct dse_stats {
   double lane0_kernel_ms;     /* the timed launches of stream ("lane") 0 alone: summed HIP-event */
   double lane0_launches;      /* time, their count and their amplitudes x terms -- in persistent */
   double lane0_amp_terms;     /* mode lane 0 holds the 2-tile registers (the critical stream)    */
+  double matrix_build_ms;     /* propagator-matrix mode (mode 5): HIP-event time of the column   */
+  double matrix_products_ms;  /* build of U (k_ucols) and of all products psi_{j+1} = U psi_j    */
+  double matrix_products;     /* (k_symv + k_symv_reduce, or zgemv), their count, and the        */
+  double matrix_bytes_per_product; /* bytes one product reads (U's stored tiles + x; ABI 10)     */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */

@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 9
+DSE_ABI_VERSION = 10
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -65,6 +65,10 @@ class DseStats(C.Structure):
         ("lane0_kernel_ms", C.c_double),
         ("lane0_launches", C.c_double),
         ("lane0_amp_terms", C.c_double),
+        ("matrix_build_ms", C.c_double),
+        ("matrix_products_ms", C.c_double),
+        ("matrix_products", C.c_double),
+        ("matrix_bytes_per_product", C.c_double),
     ]
 
     def as_dict(self):

@@ -226,6 +226,7 @@ struct dse_ctx {
   // option "symv_fused": each product's reduction inside the product's launch (agent-scope counters
   // with a release per workgroup): measured 22.9 vs 10.4 ms for config 2, so off by default
   int symv_fused = 0;
+  double mx_build_ms = 0.0, mx_products_ms = 0.0, mx_products = 0.0, mx_bytes_per_product = 0.0;  // last matrix_run
 
   // spanning registers (dse_span.hip): option "span" 0 off; s = 1..4: every register that fits
   // runs over 2^s workgroups (one per CU) of 2^(n - s) amplitudes; "span_rb": amplitudes per
@@ -2272,6 +2273,17 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
   HIPC(hipMemsetAsync(d_err, 0, sizeof(int), st));
   HIPC(hipMemsetAsync(d_cnt, 0, nb * sizeof(int), st));
   DevArena ar;  // complex build only: the basis columns
+  // HIP events: build | products | (observables), read back for dse_stats (matrix_*)
+  hipEvent_t mev[3] = {nullptr, nullptr, nullptr};
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      for (int i = 0; i < 3; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } mev_guard{mev};
+  for (auto& e : mev) HIPC(hipEventCreate(&e));
+  HIPC(hipEventRecord(mev[0], st));
   if (real_build) {
     double* d_cf = reinterpret_cast<double*>(base + oCoef);
     HIPC(hipMemcpyAsync(d_cf, cf.data(), cf.size() * sizeof(double), hipMemcpyHostToDevice, st));
@@ -2310,6 +2322,7 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
     HIPC(launch_basis_init(d_init, (int)dim, dim, st));
     HIPC(launch_interval(P.L, P.imag, d_p, d_items, (int)dim, 0, 0, 1, d_err, d_err, st, (long)dim));
   }
+  HIPC(hipEventRecord(mev[1], st));
   // psi_0 = e_x0, psi_1 = U e_x0 (column x0), psi_{j+1} = U psi_j
   HIPC(hipMemsetAsync(S, 0, dim * sizeof(double2), st));
   static const double2 one_c = {1.0, 0.0};
@@ -2334,6 +2347,7 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
     if (rs != rocblas_status_success)
       return fail(ctx, DSE_ERR_HIP, "rocblas zgemv failed (status " + std::to_string((int)rs) + ")");
   }
+  HIPC(hipEventRecord(mev[2], st));
   DenseProb D = {};
   D.n = n;
   D.rot = 0;
@@ -2355,6 +2369,13 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
     finish_obs(P, h.data() + (size_t)ti * 8, obs_out + (size_t)pi * DSE_N_OBS * n_t + ti, (size_t)n_t);
   P.degree = deg;
   *h_apps = (double)deg * (double)dim;
+  float b_ms = 0.f, p_ms = 0.f;
+  HIPC(hipEventElapsedTime(&b_ms, mev[0], mev[1]));
+  HIPC(hipEventElapsedTime(&p_ms, mev[1], mev[2]));
+  ctx->mx_build_ms = b_ms;
+  ctx->mx_products_ms = p_ms;
+  ctx->mx_products = (double)std::max(0, n_t - 2);
+  ctx->mx_bytes_per_product = (double)(u_elems * sizeof(double2) + dim * sizeof(double2));
   return DSE_OK;
 }
 
@@ -3358,6 +3379,12 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->lane0_kernel_ms = lane0_ms;
     stats->lane0_launches = lane0_launches;
     stats->lane0_amp_terms = lane0_amps;
+    if (matrix_pi >= 0) {
+      stats->matrix_build_ms = ctx->mx_build_ms;
+      stats->matrix_products_ms = ctx->mx_products_ms;
+      stats->matrix_products = ctx->mx_products;
+      stats->matrix_bytes_per_product = ctx->mx_bytes_per_product;
+    }
   }
   return DSE_OK;
 }

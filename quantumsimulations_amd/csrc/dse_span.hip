@@ -66,7 +66,7 @@ struct SpanGeo {
   static constexpr int NPI = (TB * (TB - 1) / 2 + TB - 1) / TB;  // thread pairs per iteration
   static constexpr int IW = (8 + NPI + 1) / 2;         // dv2 per coefficient row (span_row_dv2)
   static constexpr uint32_t TBYTES = (16u << L);
-  static constexpr int US = R <= 4 ? 4 : 2;            // u operands built per pre-pass sweep
+  static constexpr int US = (R <= 4 && NT < 1024) ? 4 : 2;  // u operands built per pre-pass sweep
 };
 
 // The canonical thread-pair schedule of k_span: pair p = (a, b), a < b < TB, enumerated
@@ -137,7 +137,10 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
        const int2* __restrict__ items, int q, int set, int n_out, int* __restrict__ err) {
   using G = SpanGeo<L, RB>;
   constexpr int R = G::R, TB = G::TB, NT = G::NT, IW = G::IW, NPI = G::NPI, US = G::US;
-  constexpr int NB = R <= 4 ? 4 : 3;         // operands loaded together in phase 4
+  // 1024-thread tiles run 4 waves per SIMD (<= 128 VGPRs): fewer operands in flight, propagator
+  // sums loaded when used
+  constexpr bool LEAN = NT >= 1024;
+  constexpr int NB = LEAN ? 2 : (R <= 4 ? 4 : 3);  // operands loaded together in phase 4
   constexpr int J_PUB = TB > 2 ? 2 : TB - 1;  // loop iteration that publishes the term
   constexpr uint32_t TBYTES = G::TBYTES;
   __shared__ SpanShared<L, RB> S;
@@ -412,7 +415,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       accr[j] = (j == n_out - 1) ? acc_t
                                  : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << P.n) + ((size_t)h << L), TBYTES);
       if (ab & 16) upd[j] = false;
-      if (upd[j] && k > 1) {
+      if (!LEAN && upd[j] && k > 1) {
 #pragma unroll
         for (int r = 0; r < R; ++r) av[j][r] = bld(accr[j], voff, (uint32_t)(r * NT * 16));
       }
@@ -495,6 +498,10 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
       if (!upd[j]) continue;
+      if (LEAN && k > 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) av[j][r] = bld(accr[j], voff, (uint32_t)(r * NT * 16));
+      }
       const int nt = coef_nterm(k, dj[j]);
       const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);
       const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
