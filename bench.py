@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--mixed-launch", type=int, default=int(os.environ.get("DSE_MIXED_LAUNCH", "1")),
                     help="persistent mode: 1- and 2-tile problems in one launch per interval (1, default) "
                     "or one stream each (0)")
+    ap.add_argument("--real", type=int, default=int(os.environ.get("DSE_REAL", "1")),
+                    help="real-component mode (dse_real.hip) for the 13/14-qubit registers (0: k_interval)")
     ap.add_argument("--obs-overlap", type=int, default=int(os.environ.get("DSE_OBS_OVERLAP", "0")),
                     help="persistent mode: observables on a second stream per lane (1)")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
@@ -591,6 +593,7 @@ def main():
     eng.set_option("outputs_per_launch", args.outputs_per_launch)
     eng.set_option("mixed_launch", args.mixed_launch)
     eng.set_option("obs_overlap", args.obs_overlap)
+    eng.set_option("real", args.real)
     if os.environ.get("DSE_CORESIDENT"):  # diagnostics: workgroups per 2-tile interval launch chunk
         eng.set_option("coresident", float(os.environ["DSE_CORESIDENT"]))
     for p in probs:

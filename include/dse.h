@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 10
+#define DSE_ABI_VERSION 11
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -111,6 +111,8 @@ typedef struct dse_stats {
   double matrix_products_ms;  /* build of U (k_ucols) and of all products psi_{j+1} = U psi_j    */
   double matrix_products;     /* (k_symv + k_symv_reduce, or zgemv), their count, and the        */
   double matrix_bytes_per_product; /* bytes one product reads (U's stored tiles + x; ABI 10)     */
+  int32_t real_problems;      /* registers run as two real recurrences in the rotated frame      */
+  int32_t reserved1;          /* (k_real, option "real"; ABI 11)                                 */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */

@@ -69,6 +69,8 @@ struct alignas(16) CoefK {
   int pad[3];
 };
 
+struct RealTab;
+
 struct DevProb {
   double2* buf[3];
   const double* zzlo;     // [2^L]  sum_{i<j<L} zz_ij s_i s_j
@@ -110,6 +112,11 @@ struct DevProb {
   double2* xacc;
   int n_acc;
   int xacc_q;             // 0, or n_acc - 1: intermediate outputs per launch-parity set
+  // real-component mode (dse_real.hip): the register's tables, its [a | b] input and the
+  // per-output, per-component propagator sums
+  const struct RealTab* rtab;
+  double* rin;
+  double2* racc;
 };
 
 // ---- spanning registers (dse_span.hip): one register over 2^s cooperating workgroups ----------
@@ -118,7 +125,7 @@ struct DevProb {
 // CUs.  In a tile, thread t of NT = 2^(L - RB) owns the R = 2^RB amplitudes x = r * NT + t.
 constexpr int kSpanMaxTop = 4;   // top (tile-index) bits: up to 16 workgroups per register
 constexpr int kSpanWaves = 16;   // hand-off flags per tile: one per wave (<= 1024 threads)
-constexpr int kSpanMaxIt = 160;  // fused-loop coefficient rows (dv2): TB x (8 + pairs per iteration) / 2
+constexpr int kSpanMaxIt = 160;  // fused-loop iteration rows (dv2): TB x (4 + pairs per iteration)
 constexpr int kSpanMaxOps = kSpanMaxTop + kSpanMaxTop * (kSpanMaxTop - 1) / 2;
 // One cross-tile operand of every tile's H application (phase 4 of k_span):
 //   kind 0  u_b of the partner h ^ e_b (its slot b): flip_b w + sum_j g_jb [x_j == h_b] w(x ^ e_j)
@@ -137,9 +144,8 @@ struct alignas(16) SpanTab {
   SpanOp ops[kSpanMaxOps];
   int rflip_mask, u_mask, n_ops, need_raw;  // need_raw: some operand reads a partner's raw w
   int n_it, pad[3];
-  // coefficient row of iteration j (thread bit j), as doubles: c0i c1i c0r c1r (drive of j by the
-  // output value t_j), g of the pairs (j, register bit 0..3), then g of the iteration's thread pairs
-  // in the canonical schedule (dse_span.hip span_pair_mask)
+  // iteration j (thread bit j): [0] re0 im0, [1] re1 im1 (drive of j by output value t_j),
+  // [2] [3] pairs (j, register bit 0..3), [4 + q] thread pair q of the iteration (mask bits, g)
   double2 it[kSpanMaxIt];
 };
 struct SpanDesc {
@@ -155,6 +161,40 @@ bool span_supported(int L, int RB);
 hipError_t set_span_spin_limit(int limit);
 hipError_t set_span_ablate(int mask);
 hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu);
+
+// ---- real-component registers (dse_real.hip) ------------------------------------------------
+// With every drive purely imaginary (the sweep's phase pi/2) H' = D H D^dagger, D|x> = i^|x| |x>, is
+// REAL symmetric, so T_k(H') maps real vectors to real vectors: the rotated state phi = a + i b
+// evolves as two independent real Chebyshev recurrences, T_k(H~') a and T_k(H~') b, whose complex
+// propagator sums acc_c = sum_k c_k T_k c give phi(t + tau) = acc_a + i acc_b.  One workgroup per
+// real component holds the WHOLE register in LDS (2^14 x 8 B = 128 KiB): no cross-workgroup
+// hand-off inside a launch.  Thread t of 512 owns rows x = r * 512 + t, r < R = 2^(n - 9).
+constexpr int kRealRB = 5;                  // register bits at n = 14 (R = 32 rows per thread)
+constexpr int kRealRegPairs = kRealRB * (kRealRB - 1) / 2;
+__host__ __device__ constexpr int real_rr_index(int a, int b) {  // a < b < kRealRB
+  return a * (2 * kRealRB - a - 1) / 2 + (b - a - 1);
+}
+struct alignas(16) RealTab {
+  double rr_g[kRealRegPairs];  // rotated pair coefficients (-g) among register bits
+  double rflip[kRealRB][2];    // rotated drive of register bit i, by output value (0, 1)
+  uint64_t x0;                 // psi(t0) = e_x0
+  int x0pop;                   // popcount(x0): psi = i^{|x0| - |x|} phi
+  int rflip_mask;
+  // coefficient row of iteration j (thread bit j), as doubles: the rotated drive of j by output
+  // value (2), the rotated pairs (j, register bit 0..5) (6), the iteration's 4 thread pairs in the
+  // canonical schedule (span_pair_mask) (4)
+  double2 it[9 * 6];
+};
+// real_c (per problem, real mode): rin = [a | b] (2 x 2^n doubles), racc = [output j][component c]
+// blocks of 2^n complex propagator sums
+hipError_t launch_real(const DevProb* probs, const int2* items, int n_items, int set, int n_out,
+                       hipStream_t st);
+// psi = i^{|x0| - |x|} (acc_a + i acc_b) of every output (into the state buffer / intermediate
+// outputs k_obs reads) and, from the last output, the next interval's [a | b]
+hipError_t launch_real_combine(const DevProb* probs, const int2* items, int n_items, int q, int n_out,
+                               hipStream_t st);
+hipError_t real_occupancy(int* blocks_per_cu);
+hipError_t launch_real_init(const DevProb* probs, const int2* items, int n_items, hipStream_t st);
 
 // Coefficient row of output j of offset set `set`: kcap1 + 1 entries, row[0].x = the degree d of
 // that output's series, row[1 + k] = a_k for k = 0..d (zero beyond): 16 B per term.

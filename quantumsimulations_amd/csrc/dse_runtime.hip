@@ -93,6 +93,8 @@ struct HostProblem {
   // spanning register (dse_span.hip): this evolve runs the register over 2^span_s workgroups of
   // 2^(n - span_s) amplitudes (0: not spanned)
   int span_s = 0;
+  // real-component mode (dse_real.hip): this evolve runs the register as two real recurrences
+  bool rl = false;
 };
 
 // One stream's share of the problems, grouped by tile size.
@@ -110,6 +112,10 @@ struct LaneGroup {
   // span_off in dse_ctx::d_span_items (tiles of one register 8 apart, padding items x = -1)
   int span_L = 0, span_rb = 0;
   int64_t span_off = 0, span_count = 0;
+  // real-component registers: k_real over real_count items (problem, component) from real_off in
+  // dse_ctx::d_real_items, then k_real_combine over real_np items (problem, 0) from real_poff
+  bool real = false;
+  int64_t real_off = 0, real_count = 0, real_poff = 0, real_np = 0;
 };
 struct Lane {
   hipStream_t stream = nullptr;
@@ -233,6 +239,15 @@ struct dse_ctx {
   // thread 2^span_rb (0: 512 threads per workgroup)
   int span = 0;
   int span_tile = 0;                // option "span_tile" L > 0: every register of n > L qubits spans 2^(n-L) tiles
+  // real-component mode (dse_real.hip, option "real", default 1): registers of 13 or 14 qubits with
+  // imaginary drives run as two real recurrences, one workgroup per component, no hand-off
+  int real_mode = 1;
+  unsigned char* d_real = nullptr;  // [a | b] inputs and propagator sums of the real-mode registers
+  size_t real_cap = 0;
+  unsigned char* d_real_tab = nullptr;
+  size_t real_tab_cap = 0;
+  int2* d_real_items = nullptr;
+  size_t real_items_cap = 0;
   int span_rb = 0;
   SpanDesc* d_span = nullptr;       // per problem
   size_t span_cap = 0;
@@ -427,6 +442,10 @@ void free_device(dse_ctx* ctx) {
   if (ctx->d_xacc) (void)hipFree(ctx->d_xacc), ctx->d_xacc = nullptr;
   ctx->xacc_cap = 0;
   if (ctx->d_span) (void)hipFree(ctx->d_span), ctx->d_span = nullptr;
+  if (ctx->d_real) (void)hipFree(ctx->d_real), ctx->d_real = nullptr;
+  if (ctx->d_real_tab) (void)hipFree(ctx->d_real_tab), ctx->d_real_tab = nullptr;
+  if (ctx->d_real_items) (void)hipFree(ctx->d_real_items), ctx->d_real_items = nullptr;
+  ctx->real_cap = ctx->real_tab_cap = ctx->real_items_cap = 0;
   if (ctx->d_span_tab) (void)hipFree(ctx->d_span_tab), ctx->d_span_tab = nullptr;
   if (ctx->d_span_slots) (void)hipFree(ctx->d_span_slots), ctx->d_span_slots = nullptr;
   if (ctx->d_span_flags) (void)hipFree(ctx->d_span_flags), ctx->d_span_flags = nullptr;
@@ -1358,6 +1377,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "span") {  // spanning registers: 0 off, 1..4 top bits (workgroups 2^s per register)
     if (!(value >= 0 && value <= kSpanMaxTop)) return fail(ctx, DSE_ERR_ARG, "span must be in 0..4");
     ctx->span = (int)value;
+  } else if (k == "real") {  // real-component mode for registers of 13 / 14 qubits (imaginary drives)
+    ctx->real_mode = value != 0.0;
   } else if (k == "span_tile") {  // spanning registers: tile bits L (0 off); n > L qubits span 2^(n-L) tiles
     if (!(value == 0 || (value >= 10 && value <= 13))) return fail(ctx, DSE_ERR_ARG, "span_tile must be 0 or in 10..13");
     ctx->span_tile = (int)value;
@@ -2473,25 +2494,21 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
   const int n = P.n;
   const int TB = L - RB;
   const int npi = (TB * (TB - 1) / 2 + TB - 1) / TB;
-  const int iw = (8 + npi + 1) / 2;  // dv2 per coefficient row (dse_span.hip SpanGeo::IW)
+  const int iw = 4 + npi;
   if (TB * iw > kSpanMaxIt || L > 16 || RB > 4 || s > kSpanMaxTop || n != L + s) return DSE_ERR_ARG;
   std::memset(&T, 0, sizeof(T));
   T.n_it = TB * iw;
-  // row j as doubles: c0i c1i c0r c1r (drive of thread bit j by output value), g with register
-  // bits 0..3, then the thread pairs of iteration j in the canonical schedule (span_pair_mask)
-  auto row = [&](int j, int e) -> double& {
-    double2& d = T.it[j * iw + e / 2];
-    return (e & 1) ? d.y : d.x;
-  };
+  auto it = [&](int j, int e) -> double2& { return T.it[j * iw + e]; };
+  std::vector<std::pair<uint32_t, double>> tpairs;
   for (int i = 0; i < n; ++i)
     for (int j = i + 1; j < n; ++j) {
       const double g = P.pair[i * n + j];
       if (g == 0.0) continue;
-      if (j < TB) {  // canonical index of (i, j): lexicographic over a < b < TB
-        const int p = i * TB - i * (i + 1) / 2 + (j - i - 1);
-        row(p / npi, 8 + p % npi) = g;
+      if (j < TB) {
+        tpairs.push_back({(1u << i) | (1u << j), g});
       } else if (j < L && i < TB) {
-        row(i, 4 + (j - TB)) = g;
+        const int r = j - TB;
+        (r & 1 ? it(i, 2 + r / 2).y : it(i, 2 + r / 2).x) = g;
       } else if (j < L) {
         T.rr_g[rr_index(i - TB, j - TB)] = g;
       } else if (i < L) {
@@ -2507,6 +2524,12 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
         T.need_raw = 1;
       }
     }
+  if ((int)tpairs.size() > TB * npi) return DSE_ERR_ARG;
+  for (size_t p = 0; p < tpairs.size(); ++p) {
+    double2& e = it((int)(p / npi), 4 + (int)(p % npi));
+    e.x = __builtin_bit_cast(double, (uint64_t)tpairs[p].first);
+    e.y = tpairs[p].second;
+  }
   for (int b = 0; b < n; ++b) {
     double f[4];
     for (int c = 0; c < 4; c += 2) {  // as build_tables: cos(pi/2) residues dropped
@@ -2516,10 +2539,8 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
     }
     if (f[0] == 0.0 && f[1] == 0.0 && f[2] == 0.0 && f[3] == 0.0) continue;
     if (b < TB) {
-      row(b, 0) = f[1];
-      row(b, 1) = f[3];
-      row(b, 2) = f[0];
-      row(b, 3) = f[2];
+      it(b, 0) = make_double2(f[0], f[1]);
+      it(b, 1) = make_double2(f[2], f[3]);
     } else if (b < L) {
       for (int c = 0; c < 4; ++c) T.rflip[b - TB][c] = f[c];
       T.rflip_mask |= 1 << (b - TB);
@@ -2541,6 +2562,59 @@ int build_span_table(const HostProblem& P, int L, int RB, int s, SpanTab& T) {
       T.need_raw = 1;
     }
   }
+  return DSE_OK;
+}
+
+// ---- real-component registers (dse_real.hip) ---------------------------------------------------
+
+bool real_eligible(const HostProblem& P) {
+  return !P.side() && P.span_s == 0 && P.shard_bits == 0 && P.imag && (P.n_local == 13 || P.n_local == 14);
+}
+
+// RealTab of register P (n = 13 or 14: 9 thread bits, n - 9 register bits): the coefficients of
+// H' = D H D^dagger, D|x> = i^|x| |x>: pairs -g (i^{+-2}), drives by the output bit value v of the
+// flipped bit: v = 0 -> +Im c0, v = 1 -> -Im c1 (i^{-+1} times the imaginary coefficient, k_dense_h)
+int build_real_table(const HostProblem& P, RealTab& T) {
+  const int n = P.n, TB = 9, RB = n - TB;
+  if (RB < 4 || RB > kRealRB) return DSE_ERR_ARG;
+  std::memset(&T, 0, sizeof(T));
+  auto row = [&](int j, int e) -> double& {
+    double2& d = T.it[j * 6 + e / 2];
+    return (e & 1) ? d.y : d.x;
+  };
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j) {
+      const double g = -P.pair[i * n + j];
+      if (g == 0.0) continue;
+      if (j < TB) {  // canonical slot of (i, j): lexicographic over a < b < 9, 4 per iteration
+        const int p = i * TB - i * (i + 1) / 2 + (j - i - 1);
+        row(p / 4, 8 + p % 4) = g;
+      } else if (i < TB) {
+        row(i, 2 + (j - TB)) = g;
+      } else {
+        T.rr_g[real_rr_index(i - TB, j - TB)] = g;
+      }
+    }
+  for (int b = 0; b < n; ++b) {
+    double f[4];
+    for (int c = 0; c < 4; c += 2) {  // as build_tables: cos(pi/2) residues dropped
+      f[c] = P.flip[4 * b + c];
+      f[c + 1] = P.flip[4 * b + c + 1];
+      if (std::fabs(f[c]) <= 1e-15 * std::hypot(f[c], f[c + 1])) f[c] = 0.0;
+    }
+    if (f[0] != 0.0 || f[2] != 0.0) return DSE_ERR_ARG;  // not an imaginary drive
+    if (f[1] == 0.0 && f[3] == 0.0) continue;
+    if (b < TB) {
+      row(b, 0) = f[1];
+      row(b, 1) = -f[3];
+    } else {
+      T.rflip[b - TB][0] = f[1];
+      T.rflip[b - TB][1] = -f[3];
+      T.rflip_mask |= 1 << (b - TB);
+    }
+  }
+  T.x0 = P.psi0;
+  T.x0pop = __builtin_popcountll(P.psi0);
   return DSE_OK;
 }
 
@@ -2625,6 +2699,17 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   }
   if (!persistent)
     for (auto& P : ctx->probs) P.span_s = 0;
+  // real-component mode: when every Chebyshev register qualifies (one launch kind per interval)
+  {
+    bool real_mode = persistent && ctx->real_mode && !ctx->obs_overlap;
+    int n_cheb = 0;
+    for (auto& P : ctx->probs) {
+      if (P.side()) continue;
+      ++n_cheb;
+      real_mode = real_mode && real_eligible(P);
+    }
+    for (auto& P : ctx->probs) P.rl = real_mode && n_cheb > 0 && !P.side();
+  }
   // streaming: registers of more than one 2^13 tile take the Walsh-Hadamard engine (option wht)
   bool used_wht = false;
   bool any_dist_step = any_dist;  // dist shards on the step kernels: per-term shard exchange
@@ -2794,6 +2879,46 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       if (use) off += xsets * ((size_t)(M - 1) << ctx->probs[pi].n_local);
     }
   }
+  // real-component registers: tables, [a | b] inputs and per-output, per-component sums
+  {
+    Arena tabs;
+    std::vector<size_t> tab_off(ctx->probs.size(), 0);
+    size_t need = 0;  // in double2 units
+    for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+      const HostProblem& P = ctx->probs[pi];
+      ctx->h_desc[pi].rtab = nullptr;
+      ctx->h_desc[pi].rin = nullptr;
+      ctx->h_desc[pi].racc = nullptr;
+      if (!P.rl) continue;
+      RealTab T;
+      if ((rc = build_real_table(P, T)) != DSE_OK) return fail(ctx, rc, "real-mode tables: drives not imaginary");
+      tab_off[pi] = tabs.add(&T, sizeof(T));
+      need += ((size_t)1 + 2 * (size_t)M) << P.n_local;
+    }
+    if (need > 0) {
+      if ((rc = upload_arena(ctx, tabs, &ctx->d_real_tab, &ctx->real_tab_cap, ctx->lanes[0].stream))) return rc;
+      HIPC(hipStreamSynchronize(ctx->lanes[0].stream));
+      if (need * sizeof(double2) > ctx->real_cap) {
+        if (ctx->d_real) (void)hipFree(ctx->d_real), ctx->d_real = nullptr;
+        ctx->real_cap = 0;
+        if (hipMalloc(&ctx->d_real, need * sizeof(double2)) != hipSuccess)
+          return fail(ctx, DSE_ERR_OOM, "real-mode buffer allocation failed (" +
+                                            std::to_string(need * sizeof(double2)) + " bytes)");
+        ctx->real_cap = need * sizeof(double2);
+      }
+      double2* base = reinterpret_cast<double2*>(ctx->d_real);
+      size_t off = 0;
+      for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+        const HostProblem& P = ctx->probs[pi];
+        if (!P.rl) continue;
+        DevProb& d = ctx->h_desc[pi];
+        d.rtab = reinterpret_cast<const RealTab*>(ctx->d_real_tab + tab_off[pi]);
+        d.rin = reinterpret_cast<double*>(base + off);  // [a | b]: 2 x 2^n doubles
+        d.racc = base + off + ((size_t)1 << P.n_local);
+        off += ((size_t)1 + 2 * (size_t)M) << P.n_local;
+      }
+    }
+  }
 
   // ---- lanes ----
   // persistent: 2-tile problems on lane 0 (their workgroup pairs must be co-resident), 1-tile
@@ -2915,9 +3040,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     const bool mixed = mixed_L(P);
     // tiles 0: a mixed group; < 0: spanning registers, -(16 L_span + rb)
     const int Ls = P.n_local - P.span_s;
-    const std::pair<int, int64_t> key(P.L, P.span_s ? -(16 * Ls + span_rb_for(ctx, Ls)) : (mixed ? 0 : P.n_tiles));
+    const std::pair<int, int64_t> key(P.L, P.rl ? -1000 : P.span_s ? -(16 * Ls + span_rb_for(ctx, Ls))
+                                                                : (mixed ? 0 : P.n_tiles));
     int lane = (int)(i % n_lanes);
-    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1 || mixed || P.span_s) ? 0 : 1;
+    if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1 || mixed || P.span_s || P.rl) ? 0 : 1;
     // shards of one register read each other's vectors: same lane, hence the same launches
     if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);
@@ -2935,6 +3061,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       LaneGroup g;
       g.L = kv.first.first;
       g.tiles = (int)kv.first.second;
+      g.real = g.tiles == -1000;
+      if (g.real) g.tiles = 1;  // no hand-off flags, no pair placement
       if (g.tiles < 0) g.span_L = (-g.tiles) / 16, g.span_rb = (-g.tiles) % 16;
       g.off = (int64_t)items.size();
       for (int pi : kv.second) {  // already in degree order
@@ -3056,6 +3184,34 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
         }
         g.span_count = (int64_t)sitems.size() - g.span_off;
       }
+    // real-component groups: items (problem, component) in degree order, then (problem, 0) per
+    // problem for the combine launch
+    std::vector<int2> ritems;
+    for (auto& ln : ctx->lanes)
+      for (auto& g : ln.groups) {
+        if (!g.real) continue;
+        std::vector<int> pis;
+        for (int64_t i = 0; i < g.count; ++i) {
+          const int2 e = items[g.off + i];
+          if (pis.empty() || pis.back() != e.x) pis.push_back(e.x);
+        }
+        g.real_off = (int64_t)ritems.size();
+        for (int pi : pis) ritems.push_back(make_int2(pi, 0)), ritems.push_back(make_int2(pi, 1));
+        g.real_count = (int64_t)ritems.size() - g.real_off;
+        g.real_poff = (int64_t)ritems.size();
+        for (int pi : pis) ritems.push_back(make_int2(pi, 0));
+        g.real_np = (int64_t)pis.size();
+      }
+    if (!ritems.empty()) {
+      if (ritems.size() > ctx->real_items_cap) {
+        if (ctx->d_real_items) (void)hipFree(ctx->d_real_items), ctx->d_real_items = nullptr;
+        ctx->real_items_cap = 0;
+        if (hipMalloc(&ctx->d_real_items, ritems.size() * sizeof(int2)) != hipSuccess)
+          return fail(ctx, DSE_ERR_OOM, "real item allocation failed");
+        ctx->real_items_cap = ritems.size();
+      }
+      HIPC(hipMemcpy(ctx->d_real_items, ritems.data(), ritems.size() * sizeof(int2), hipMemcpyHostToDevice));
+    }
     if (!sitems.empty()) {
       if (sitems.size() > ctx->span_items_cap) {
         if (ctx->d_span_items) (void)hipFree(ctx->d_span_items), ctx->d_span_items = nullptr;
@@ -3114,6 +3270,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       for (size_t i0 = 0; i0 < init.size(); i0 += 65535)
         HIPC(launch_basis_init(ctx->d_init + i0, (int)std::min<size_t>(65535, init.size() - i0), max_amps, st0));
     }
+    for (auto& ln : ctx->lanes)  // real-component registers: [a | b] = [e_x0 | 0]
+      for (auto& g : ln.groups)
+        if (g.real) HIPC(launch_real_init(ctx->d_probs, ctx->d_real_items + g.real_poff, (int)g.real_np, st0));
     HIPC(hipStreamSynchronize(st0));
   }
   double small_happl = 0.0, small_launches = 0.0;
@@ -3217,6 +3376,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
           if (g.tiles < 0) HIPC(hipMemsetAsync(ctx->d_span_flags, 0, ctx->span_flag_cap, ln.stream));
           else if (g.tiles != 1) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
           auto launch_g = [&](int64_t off, int cnt) -> hipError_t {
+            if (g.real)
+              return launch_real(ctx->d_probs, ctx->d_real_items + g.real_off, (int)g.real_count, set, G.n_out,
+                                 ln.stream);
             if (g.tiles < 0)
               return launch_span(g.span_L, g.span_rb, imag_all, ctx->d_probs, ctx->d_span, ctx->d_span_items + g.span_off,
                                  (int)g.span_count, q, set, G.n_out, d_err, ln.stream);
@@ -3246,6 +3408,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
             amp_updates += am;
             all_flops += fl;
           }
+          // real-component registers: psi of every output (computational frame) and the next [a | b]
+          if (g.real)
+            HIPC(launch_real_combine(ctx->d_probs, ctx->d_real_items + g.real_poff, (int)g.real_np, q, G.n_out,
+                                     ln.stream));
           continue;
         }
         if (any_dist_step && (rc = dist_exchange(ctx, q ? 2 : 0, 1, ln.stream))) return rc;
@@ -3358,6 +3524,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     int n_span = 0;
     for (auto& P : ctx->probs) n_span += P.span_s ? 1 : 0;
     stats->span_problems = n_span;
+    int n_real = 0;
+    for (auto& P : ctx->probs) n_real += P.rl ? 1 : 0;
+    stats->real_problems = n_real;
     stats->dense_ms = dense_ms;
     stats->dense_eig_ms = dense_eig_ms;
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;

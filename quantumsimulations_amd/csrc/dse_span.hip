@@ -30,7 +30,6 @@
 // Ring of kXSlots slots per operand kind: slot (k - 1) % kXSlots carries the operand of term k,
 // rewritten kXSlots terms later, by when every reader has passed its flag of a later term.
 #include <type_traits>
-#include <utility>
 
 #include "dse_device.h"
 
@@ -64,33 +63,10 @@ struct SpanGeo {
   static constexpr int NT = 1 << TB;                   // threads per workgroup
   static constexpr int NW = NT / 64;                   // waves
   static constexpr int NPI = (TB * (TB - 1) / 2 + TB - 1) / TB;  // thread pairs per iteration
-  static constexpr int IW = (8 + NPI + 1) / 2;         // dv2 per coefficient row (span_row_dv2)
+  static constexpr int IW = 4 + NPI;                   // dv2 per iteration row
   static constexpr uint32_t TBYTES = (16u << L);
   static constexpr int US = (R <= 4 && NT < 1024) ? 4 : 2;  // u operands built per pre-pass sweep
 };
-
-// The canonical thread-pair schedule of k_span: pair p = (a, b), a < b < TB, enumerated
-// lexicographically, runs in iteration p / NPI, slot p % NPI (the host's span_pair_slot).
-__host__ __device__ constexpr uint32_t span_pair_mask(int TB, int j, int q) {
-  const int np = TB * (TB - 1) / 2, npi = (np + TB - 1) / TB;
-  int p = j * npi + q;
-  if (q >= npi || p >= np) return 0u;
-  int a = 0;
-  while (p >= TB - 1 - a) {
-    p -= TB - 1 - a;
-    ++a;
-  }
-  return (1u << a) | (1u << (a + 1 + p));
-}
-
-template <typename F, int... J>
-__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, J...>) {
-  (f(std::integral_constant<int, J>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
 
 template <bool IMAG>
 __device__ __forceinline__ double2 smad(double2 acc, double cr, double ci, double2 s) {
@@ -326,80 +302,56 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
         }
     }
 
-    // ---- fused loop over the thread bits, unrolled: iteration j reads the sweep partner t ^ e_j
-    // (its drive and its pairs with the register bits) and the iteration's share of the thread-bit
-    // pairs, whose masks are compile-time (span_pair_mask: the canonical schedule the host's
-    // coefficient rows follow); wave bits (j >= 6) take scalar branches instead of zero
-    // coefficients.  The term is published at iteration J_PUB (per wave: s_waitcnt vmcnt(0), then
-    // one lane's flag store), so the pre-pass's stores drain under the loop ----
-    const bool pub = u_mask || (need_raw && k > 1);
+    // ---- fused loop over the thread bits: the sweep's partner rows, then the thread pairs one at a
+    // time, each next partner's rows in flight under the current one's FMAs ----
     const uint32_t itb = lds_byte(&S.it[0][0]);
-    uint32_t ia0;  // one VGPR base for the coefficient rows (broadcast reads, immediate offsets)
-    asm volatile("v_mov_b32_e32 %0, %1" : "=v"(ia0) : "s"(itb));
+    // publish term k -- u(w_{k-1}) stored by the pre-pass, raw w_{k-1} at the end of term k - 1 --
+    // after J_PUB iterations, so the stores drain under the loop: per wave, s_waitcnt vmcnt(0)
+    // then one lane's flag store
+    const bool pub = u_mask || (need_raw && k > 1);
 #pragma unroll 1
     for (int j = 0; j < ((ab & 32) ? 0 : TB); ++j) {
       if (j == J_PUB && pub && !(ab & 2)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      uint32_t ia;  // one VGPR base for the iteration row (broadcast reads)
+      asm("v_mov_b32_e32 %0, %1" : "=v"(ia) : "s"(itb + (uint32_t)j * IW * 16u));
+      const dv2 d0 = *(ldv2*)(size_t)ia, d1 = *(ldv2*)(size_t)(ia + 16u);
       double2 pv[R];
       rows_lds<NT, R>(cur, tid ^ (1 << j), pv);
-      const uint32_t ia = ia0 + (uint32_t)(j * IW) * 16u;
-      const dv2 dI = *(ldv2*)(size_t)ia;  // (c0i, c1i)
-      const dv2 gR = *(ldv2*)(size_t)(ia + 32u);  // pairs (j, register bit 0, 1)
-      dv2 dR, gR2;
-      if (!IMAG) dR = *(ldv2*)(size_t)(ia + 16u);
-      if (RB > 2) gR2 = *(ldv2*)(size_t)(ia + 48u);
-      auto greg = [&](int i) { return i == 0 ? gR.x : i == 1 ? gR.y : i == 2 ? gR2.x : gR2.y; };
-      if (j < 6) {  // a lane bit: the output value t_j varies across the wave
-        const int bj = (tid >> j) & 1;
-        const double ci = bj ? dI.y : dI.x, cr = IMAG ? 0.0 : (bj ? dR.y : dR.x);
+      dv2 pr = *(ldv2*)(size_t)(ia + 16u * 4);
+      double2 ta[R], tb[R];
+      rows_lds<NT, R>(cur, tid ^ (int)(uint32_t)__double_as_longlong(pr.x), ta);
+      const int bj = (tid >> j) & 1;
+      const double cr = bj ? d1.x : d0.x, ci = bj ? d1.y : d0.y;
 #pragma unroll
-        for (int r = 0; r < R; ++r) out[r] = smad<IMAG>(out[r], cr, ci, pv[r]);
+      for (int r = 0; r < R; ++r) out[r] = smad<IMAG>(out[r], cr, ci, pv[r]);
+      {
+        const dv2 g01 = *(ldv2*)(size_t)(ia + 16u * 2);
+        const dv2 g23 = *(ldv2*)(size_t)(ia + 16u * 3);
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
-          const double g = greg(i), g0 = bj ? 0.0 : g, g1 = bj ? g : 0.0;
+          const double g = i == 0 ? g01.x : i == 1 ? g01.y : i == 2 ? g23.x : g23.y;
+          const double g0 = bj ? 0.0 : g, g1 = bj ? g : 0.0;
 #pragma unroll
           for (int r = 0; r < R; ++r) rfma(out[r], ((r >> i) & 1) ? g1 : g0, pv[r ^ (1 << i)]);
         }
-      } else {  // a wave bit: t_j uniform, only the rows with r_i == t_j take pair (j, i)
-        auto sweep_u = [&](auto bj_tag) {
-          constexpr int BJ = decltype(bj_tag)::value;
-          const double ci = BJ ? dI.y : dI.x, cr = IMAG ? 0.0 : (BJ ? dR.y : dR.x);
-#pragma unroll
-          for (int r = 0; r < R; ++r) out[r] = smad<IMAG>(out[r], cr, ci, pv[r]);
-#pragma unroll
-          for (int i = 0; i < RB; ++i)
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-              if (((r >> i) & 1) == BJ) rfma(out[r], greg(i), pv[r ^ (1 << i)]);
-        };
-        if (__builtin_amdgcn_readfirstlane((tid >> j) & 1))
-          sweep_u(std::integral_constant<int, 1>{});
-        else
-          sweep_u(std::integral_constant<int, 0>{});
       }
-      // the iteration's thread pairs (canonical schedule), each next partner's rows in flight
-      // under the current one's FMAs
-      double2 ta[R], tb[R];
-      uint32_t m = span_pair_mask(TB, j, 0);
-      rows_lds<NT, R>(cur, tid ^ (int)m, ta);
 #pragma unroll
       for (int qq = 0; qq < NPI; ++qq) {
-        const uint32_t mn = span_pair_mask(TB, j, qq + 1);
-        if (qq + 1 < NPI && mn) rows_lds<NT, R>(cur, tid ^ (int)mn, (qq & 1) ? ta : tb);
-        if (m) {
-          const dv2 gp = *(ldv2*)(size_t)(ia + (uint32_t)(4 + qq / 2) * 16u);
-          const double g = (qq & 1) ? gp.y : gp.x;
-          const double ge = par32((uint32_t)tid & m) ? 0.0 : g;
-          const double2* tv = (qq & 1) ? tb : ta;
-#pragma unroll
-          for (int r = 0; r < R; ++r) rfma(out[r], ge, tv[r]);
+        dv2 pn;
+        if (qq + 1 < NPI) {
+          pn = *(ldv2*)(size_t)(ia + 16u * (5 + qq));
+          rows_lds<NT, R>(cur, tid ^ (int)(uint32_t)__double_as_longlong(pn.x), (qq & 1) ? ta : tb);
         }
-        m = mn;
+        const double ge = par32((uint32_t)tid & (uint32_t)__double_as_longlong(pr.x)) ? 0.0 : pr.y;
+        const double2* tv = (qq & 1) ? tb : ta;
+#pragma unroll
+        for (int r = 0; r < R; ++r) rfma(out[r], ge, tv[r]);
+        if (qq + 1 < NPI) pr = pn;
       }
     }
-
 
     if ((ab & 32) && pub && !(ab & 2)) {  // diagnostics: no loop, publish here
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

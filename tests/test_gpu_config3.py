@@ -52,8 +52,9 @@ def test_apply_h_and_observables_match_reference_n14(engine, golden, variant, de
     engine.clear()
 
 
+@pytest.mark.parametrize("real", [1, 0])
 @pytest.mark.parametrize("m", [2, 1])
-def test_production_interval_kernel_matches_reference_n14(engine, golden, m):
+def test_production_interval_kernel_matches_reference_n14(engine, golden, m, real):
     g = golden("hpsi_traces_n14.npz")
     t = g["t"]
     keys, probs = [], []
@@ -68,14 +69,17 @@ def test_production_interval_kernel_matches_reference_n14(engine, golden, m):
     assert all(np.count_nonzero(p.pair[:13, 13]) == 13 for p in probs[6:])  # shell_off: 13 pairs cross
     engine.clear()
     engine.set_option("outputs_per_launch", m)
+    engine.set_option("real", real)   # 1 (default): k_real, two real recurrences; 0: k_interval
     try:
         for p in probs:
             engine.add(p)
         obs, st = engine.evolve(t)
     finally:
         engine.set_option("outputs_per_launch", 2)
+        engine.set_option("real", 1)
         engine.clear()
     assert st["mode"] == 1 and st["tile_bits"] == 13 and st["outputs_per_launch"] == m
+    assert st["real_problems"] == (9 if real else 0)
     worst = 0.0
     for i, key in enumerate(keys):
         for j, k in enumerate(OBS):
@@ -144,6 +148,7 @@ def test_mixed_launch_is_bitwise_identical(engine):
     for mixed in (0, 1, 1):
         engine.clear()
         engine.set_option("mixed_launch", mixed)
+        engine.set_option("real", 0)  # k_interval's launch schedule
         try:
             for variant in VARIANTS:
                 for delta in DELTAS:
@@ -151,6 +156,7 @@ def test_mixed_launch_is_bitwise_identical(engine):
             obs, st = engine.evolve(t)
         finally:
             engine.set_option("mixed_launch", 1)
+            engine.set_option("real", 1)
             engine.clear()
         assert st["mode"] == 1
         if mixed in res:

@@ -19,6 +19,15 @@ pytestmark = pytest.mark.gpu
 T = np.linspace(0.0, 2e-5, 5)
 
 
+@pytest.fixture(autouse=True)
+def _interval_kernel(engine):
+    """These tests exercise k_interval's 2-tile hand-off: the real-component mode (dse_real.hip,
+    default for these registers, no hand-off at all) is switched off for them."""
+    engine.set_option("real", 0)
+    yield
+    engine.set_option("real", 1)
+
+
 def _two_tile_problems():
     return [pb.build_problem(sweep_point_params(13, d, v, float(T[-1]), len(T)))
             for d in (0.0, 150e3) for v in ("center_on", "shell_off")]
