@@ -33,8 +33,9 @@ for T in "$@"; do
     tests)
       sel=(tests); [ -n "$arg" ] && sel=("$arg")
       [[ "$arg" == k=* ]] && sel=(tests -k "${arg#k=}")
-      timeout -k 10 1100 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu "${sel[@]}" > $OUT/gpu_tests.log 2>&1; rc=$?
-      tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || fail tests ;;
+      log=$OUT/gpu_tests${arg:+_$(basename "${arg#k=}" .py)}.log
+      timeout -k 10 1100 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu "${sel[@]}" > $log 2>&1; rc=$?
+      tail -3 $log; [ $rc -eq 0 ] || fail tests ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
       cat $OUT/smoke.log; [ $rc -eq 0 ] || fail smoke ;;
