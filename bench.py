@@ -108,10 +108,10 @@ def parse():
     return ap.parse_args()
 
 
-# rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command (tools/gpu_profile.sh +
+# rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command (tools/gpu.sh traffic +
 # tools/pmc_summary.py), newest round first
 PMC_TRAFFIC = [os.path.join(ROOT, "profiles", r, f) for r, f in
-               (("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
+               (("r04", "bench_pmc_traffic.json"), ("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
                 ("r01", "v9_pmc_traffic.json"))]
 
 
@@ -648,11 +648,14 @@ def main():
         # persistent interval kernel, priced as SURVEY.md §8(d) prices a fused Chebyshev term:
         # 80 B per amplitude (read w_{k-1}, w_{k-2}, acc; write w_k, acc) against the HBM peak
         achieved = 80.0 * amp_terms / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
-        name = f"k_interval<{args.tile_bits}, true>"
-        traffic, traffic_src = pmc_traffic(name) if args.tile_bits == 13 else (None, None)
+        real = stats[-1].get("real_problems", 0) > 0
+        name = "k_real" if real else f"k_interval<{args.tile_bits}, true>"
+        traffic, traffic_src = pmc_traffic(name) if (real or args.tile_bits == 13) else (None, None)
         fp64 = k_flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
         roof = {
-            "kernel": f"{name} (persistent Chebyshev interval: all K terms of M outputs on chip)",
+            "kernel": (f"{name} (real-component Chebyshev interval in the rotated frame: one workgroup per "
+                       "real component of a whole register, all K terms of M outputs on chip)" if real else
+                       f"{name} (persistent Chebyshev interval: all K terms of M outputs on chip)"),
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
             "traffic_source": traffic_src,
@@ -712,7 +715,9 @@ def main():
             "global_points_per_step": args.n_det if args.scaling == "strong" else len(my_det) * world,
             "evolutions_per_step_per_gpu": len(probs),
             "propagator": "exact Chebyshev (tol 1e-14)",
-            "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(mode, "streaming"),
+            "engine_mode": ({1: "persistent", 2: "walsh-hadamard"}.get(mode, "streaming")
+                            + (" real-component (k_real)" if stats[-1].get("real_problems", 0) else "")),
+            "real_problems": stats[-1].get("real_problems"),
             "tile_bits": args.tile_bits,
             "streams": args.streams,
             "outputs_per_launch": stats[-1].get("outputs_per_launch"),

@@ -177,6 +177,7 @@ def test_overlapped_observables_are_bitwise_identical(engine, m):
         engine.clear()
         engine.set_option("obs_overlap", ovl)
         engine.set_option("outputs_per_launch", m)
+        engine.set_option("real", 0)  # k_interval's schedule (obs_overlap has no real-mode form)
         try:
             for variant in VARIANTS:
                 for delta in DELTAS:
@@ -185,6 +186,7 @@ def test_overlapped_observables_are_bitwise_identical(engine, m):
         finally:
             engine.set_option("obs_overlap", 0)
             engine.set_option("outputs_per_launch", 2)
+            engine.set_option("real", 1)
             engine.clear()
         assert st["mode"] == 1 and st["outputs_per_launch"] == m
         if ovl in res:
