@@ -184,7 +184,20 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "matrix"       propagator-matrix mode for a lone register: 0 off, 1 by model
  *                         (default), 2 whenever eligible
  *          "symv_fused"   propagator-matrix mode: 1 sums each product's partials inside the
- *                         product's launch (agent-scope counters); 0 (default) a second launch */
+ *                         product's launch (agent-scope counters); 0 (default) a second launch
+ *          "real"         1 (default): registers of 13 / 14 qubits whose drives are all imaginary
+ *                         (the sweep's phase pi/2) run in the rotated frame, where H is real: two
+ *                         real Chebyshev recurrences, one workgroup each holding the whole
+ *                         register in LDS (k_real, dse_real.hip); 0: the complex kernels
+ *          "span_tile"    L > 0 (10 or 11): every register of n > L qubits runs over 2^(n - L)
+ *                         cooperating workgroups, one per CU, with per-term cross-tile hand-offs
+ *                         (k_span, dse_span.hip): a shorter chain per register for few registers
+ *                         (one simulate_rare call, one GPU's share of a strong split); 0 (default)
+ *          "span"         the same with a fixed number s = 1..4 of top bits per register
+ *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
+ *          "dense_refine" dense engine: 1 (default) eigenvalues refined by double-double
+ *                         Rayleigh quotients (exact diagonal) and output phases reduced modulo
+ *                         2 pi in double-double; 0 the eigensolver's values and fp64 phases */
 int dse_set_option(dse_ctx* ctx, const char* key, double value);
 
 /* ---- problems ----------------------------------------------------------------------------- */
