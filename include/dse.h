@@ -192,7 +192,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "span_tile"    L > 0 (10 or 11): every register of n > L qubits runs over 2^(n - L)
  *                         cooperating workgroups, one per CU, with per-term cross-tile hand-offs
  *                         (k_span, dse_span.hip): a shorter chain per register for few registers
- *                         (one simulate_rare call, one GPU's share of a strong split); 0 (default)
+ *                         (one simulate_rare call, one GPU's share of a strong split); -1
+ *                         (default): L = 11 when every Chebyshev register of the evolve is 12..15
+ *                         qubits and all their tiles fit the chip at once, else none; 0 never
  *          "span"         the same with a fixed number s = 1..4 of top bits per register
  *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
  *          "dense_refine" dense engine: 1 (default) eigenvalues refined by double-double

@@ -238,7 +238,8 @@ struct dse_ctx {
   // runs over 2^s workgroups (one per CU) of 2^(n - s) amplitudes; "span_rb": amplitudes per
   // thread 2^span_rb (0: 512 threads per workgroup)
   int span = 0;
-  int span_tile = 0;                // option "span_tile" L > 0: every register of n > L qubits spans 2^(n-L) tiles
+  int span_tile = -1;               // option "span_tile": L > 0 every register of n > L qubits spans 2^(n-L)
+                                    // tiles; -1 (default) auto: L = 11 when all tiles fit the chip at once
   // real-component mode (dse_real.hip, option "real", default 1): registers of 13 or 14 qubits with
   // imaginary drives run as two real recurrences, one workgroup per component, no hand-off
   int real_mode = 1;
@@ -1379,8 +1380,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     ctx->span = (int)value;
   } else if (k == "real") {  // real-component mode for registers of 13 / 14 qubits (imaginary drives)
     ctx->real_mode = value != 0.0;
-  } else if (k == "span_tile") {  // spanning registers: tile bits L (0 off); n > L qubits span 2^(n-L) tiles
-    if (!(value == 0 || (value >= 10 && value <= 13))) return fail(ctx, DSE_ERR_ARG, "span_tile must be 0 or in 10..13");
+  } else if (k == "span_tile") {  // spanning registers: tile bits L (0 off, -1 auto); n > L qubits span 2^(n-L) tiles
+    if (!(value == 0 || value == -1 || (value >= 10 && value <= 13)))
+      return fail(ctx, DSE_ERR_ARG, "span_tile must be -1, 0 or in 10..13");
     ctx->span_tile = (int)value;
   } else if (k == "span_rb") {  // amplitudes per thread of k_span: 2^span_rb (0: 512 threads)
     if (!(value >= 0 && value <= 3)) return fail(ctx, DSE_ERR_ARG, "span_rb must be in 0..3");
@@ -2470,18 +2472,12 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
 
 // ---- spanning registers (dse_span.hip) ------------------------------------------------------
 
+constexpr int kSpanAutoTile = 11;  // option span_tile = -1: the tile of the automatic choice
+
 // amplitudes per thread of k_span for an L-bit tile: 2^rb (option span_rb, else 512 threads)
 int span_rb_for(const dse_ctx* ctx, int L) { return ctx->span_rb > 0 ? ctx->span_rb : L - 9; }
 
-bool span_eligible(const dse_ctx* ctx, const HostProblem& P, int s);
-
-// top bits a register spans in this evolve (0: not spanned): option span_tile fixes the tile,
-// option span the number of top bits
-int span_bits(const dse_ctx* ctx, const HostProblem& P) {
-  const int s = ctx->span_tile > 0 ? P.n_local - ctx->span_tile : ctx->span;
-  return span_eligible(ctx, P, s) ? s : 0;
-}
-
+// whether register P can span its top s bits (2^s tiles of n - s bits)
 bool span_eligible(const dse_ctx* ctx, const HostProblem& P, int s) {
   if (P.side() || P.shard_bits != 0 || s < 1 || s > kSpanMaxTop) return false;
   const int L = P.n_local - s;
@@ -2689,9 +2685,32 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   for (auto& P : ctx->probs) any_big = any_big || !P.side();
   bool persistent = ctx->persistent != 0;
   bool any_dist = false;
-  // spanning registers (option span): every register that fits runs on k_span over 2^s tiles
-  for (auto& P : ctx->probs)
-    P.span_s = persistent ? span_bits(ctx, P) : 0;
+  // spanning registers (options span / span_tile): every register that fits runs on k_span over
+  // 2^s tiles.  span_tile = -1 (default, auto): when the context's registers are few enough that
+  // all their 2^11-amplitude tiles fit the chip at once (one GPU's share of a strong split, a lone
+  // simulate_rare register), a shorter chain per register; otherwise none spans
+  {
+    int tile = ctx->span_tile;
+    if (tile < 0) {
+      tile = 0;
+      int64_t wg = 0;
+      bool all = persistent && ctx->span == 0;
+      for (auto& P : ctx->probs) {
+        if (P.side()) continue;
+        const int s = P.n_local - kSpanAutoTile;
+        if (!span_eligible(ctx, P, s)) all = false;
+        wg += int64_t(1) << std::max(0, s);
+      }
+      int per_cu = 1;
+      if (all && wg > 0 && span_occupancy(kSpanAutoTile, span_rb_for(ctx, kSpanAutoTile), true, &per_cu) == hipSuccess &&
+          wg <= (int64_t)std::max(1, per_cu) * ctx->n_cu)
+        tile = kSpanAutoTile;
+    }
+    for (auto& P : ctx->probs) {
+      const int s = tile > 0 ? P.n_local - tile : ctx->span;
+      P.span_s = (persistent && span_eligible(ctx, P, s)) ? s : 0;
+    }
+  }
   for (auto& P : ctx->probs) {
     if (P.side()) continue;
     if (P.span_s == 0 && (!(interval_supported(P.L) && P.n_tiles <= 2) || P.shard_bits > 0)) persistent = false;

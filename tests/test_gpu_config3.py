@@ -70,6 +70,7 @@ def test_production_interval_kernel_matches_reference_n14(engine, golden, m, rea
     engine.clear()
     engine.set_option("outputs_per_launch", m)
     engine.set_option("real", real)   # 1 (default): k_real, two real recurrences; 0: k_interval
+    engine.set_option("span_tile", 0)  # whole registers (no automatic span)
     try:
         for p in probs:
             engine.add(p)
@@ -77,6 +78,7 @@ def test_production_interval_kernel_matches_reference_n14(engine, golden, m, rea
     finally:
         engine.set_option("outputs_per_launch", 2)
         engine.set_option("real", 1)
+        engine.set_option("span_tile", -1)
         engine.clear()
     assert st["mode"] == 1 and st["tile_bits"] == 13 and st["outputs_per_launch"] == m
     assert st["real_problems"] == (9 if real else 0)
@@ -149,6 +151,7 @@ def test_mixed_launch_is_bitwise_identical(engine):
         engine.clear()
         engine.set_option("mixed_launch", mixed)
         engine.set_option("real", 0)  # k_interval's launch schedule
+        engine.set_option("span_tile", 0)  # whole registers (no automatic span)
         try:
             for variant in VARIANTS:
                 for delta in DELTAS:
@@ -157,6 +160,7 @@ def test_mixed_launch_is_bitwise_identical(engine):
         finally:
             engine.set_option("mixed_launch", 1)
             engine.set_option("real", 1)
+            engine.set_option("span_tile", -1)
             engine.clear()
         assert st["mode"] == 1
         if mixed in res:
@@ -178,6 +182,7 @@ def test_overlapped_observables_are_bitwise_identical(engine, m):
         engine.set_option("obs_overlap", ovl)
         engine.set_option("outputs_per_launch", m)
         engine.set_option("real", 0)  # k_interval's schedule (obs_overlap has no real-mode form)
+        engine.set_option("span_tile", 0)  # whole registers (no automatic span)
         try:
             for variant in VARIANTS:
                 for delta in DELTAS:
@@ -187,6 +192,7 @@ def test_overlapped_observables_are_bitwise_identical(engine, m):
             engine.set_option("obs_overlap", 0)
             engine.set_option("outputs_per_launch", 2)
             engine.set_option("real", 1)
+            engine.set_option("span_tile", -1)
             engine.clear()
         assert st["mode"] == 1 and st["outputs_per_launch"] == m
         if ovl in res:

@@ -28,6 +28,7 @@ def _probs():
 def _run(engine, probs, real, m=2):
     engine.clear()
     engine.set_option("real", real)
+    engine.set_option("span_tile", 0)  # whole registers: 24 would span automatically
     engine.set_option("outputs_per_launch", m)
     try:
         for p in probs:
@@ -37,6 +38,7 @@ def _run(engine, probs, real, m=2):
         energies = [engine.energy(i) for i in range(len(probs))]
     finally:
         engine.set_option("real", 1)
+        engine.set_option("span_tile", -1)
         engine.set_option("outputs_per_launch", 2)
         engine.clear()
     return obs, st, states, energies

@@ -10,7 +10,9 @@ crossing drives and the pairs between two tile-index bits).
   the rare spin's drive.
 * Bitwise repeatability of the spanned evolve in one context.
 * A lone register (the reference's call pattern: simulate_rare one evolution at a time,
-  sweep_sea_detuning.py:671-673) on k_span against the default kernel.
+  sweep_sea_detuning.py:671-673) on k_span against the interval kernel (span_tile = 0).
+* The automatic policy (span_tile = -1, the default): a set whose 2^11-amplitude tiles fit the
+  chip at once spans; the bench's 192 evolutions do not.
 """
 import numpy as np
 import pytest
@@ -37,7 +39,7 @@ def _evolve(engine, probs, t, **opts):
         return engine.evolve(t)
     finally:
         engine.set_option("span", 0)
-        engine.set_option("span_tile", 0)
+        engine.set_option("span_tile", -1)
         engine.set_option("outputs_per_launch", 2)
         engine.set_option("matrix", 1)
         engine.clear()
@@ -89,8 +91,19 @@ def test_lone_spanned_register_matches_default_kernel(engine, variant, tile):
     13-qubit center_off register would take the propagator-matrix mode alone (matrix = 0 here)."""
     t = np.linspace(0.0, 1e-3, 101)
     p = pb.build_problem(_params(variant, 150e3, t))
-    ref, st0 = _evolve(engine, [p], t, matrix=0)
+    ref, st0 = _evolve(engine, [p], t, matrix=0, span_tile=0)
     obs, st = _evolve(engine, [p], t, span_tile=tile, matrix=0)
     assert st0["span_problems"] == 0 and st["span_problems"] == 1
     err = float(np.max(np.abs(obs - ref)))
     assert err < 1e-11, err
+
+
+def test_automatic_span_policy(engine):
+    """span_tile = -1 (default): the nine config-3 registers (4 + 8 + 8 tiles each) span over 2^11
+    tiles; with span_tile = 0 they run on the whole-register kernels."""
+    t = np.linspace(0.0, 1e-4, 11)
+    probs = [pb.build_problem(_params(v, d, t)) for v in VARIANTS for d in DELTAS]
+    auto, st_a = _evolve(engine, probs, t)
+    off, st_o = _evolve(engine, probs, t, span_tile=0)
+    assert st_a["span_problems"] == 9 and st_o["span_problems"] == 0
+    assert float(np.max(np.abs(auto - off))) < 1e-11
