@@ -277,6 +277,7 @@ def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, di
     best = cheb
     if dense and dense.get("full_sweep_s_extrapolated") and dense["full_sweep_s_extrapolated"] < full_s:
         best = dense
+    out["tolerance_at_t_final"] = tolerance_at_t_final(probs, best is dense, t_ref[-1], len(t_ref) - 1)
     out.update({
         "engine": "dense eigen-propagator" if best is dense else "chebyshev",
         "full_sweep_s_extrapolated": best["full_sweep_s_extrapolated"],
@@ -290,6 +291,33 @@ def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, di
                 "reference's own ZVODE trace of this grid takes ~430-1530 h per N=14 evolution on one "
                 "core (SURVEY.md §6)",
     })
+    return out
+
+
+DENSE_GROWTH_N14 = os.path.join(ROOT, "profiles", "r04", "dense_growth_n14.json")
+
+
+def tolerance_at_t_final(probs, dense: bool, t_final: float, intervals: int) -> dict:
+    """The stated accuracy of <O>(t_final) on the reference grid.  Dense engine: the fp64
+    eigenvector floor |d<O>(t)| <= 1e-10 + 1.5 eps ||H|| t, pinned at N = 7 against the mpmath
+    fixture (tests/test_gpu_grid30.py) and at N = 14 against the Chebyshev kernels over the grid's
+    first 100 intervals (tests/test_gpu_dense.py; the fitted growth rate, when its record is in
+    profiles/r04, extrapolated to t_final).  ||H|| <= the largest Gershgorin bound of the bench's
+    registers.  Chebyshev: the truncation tolerance 1e-14 per interval, summed."""
+    from quantumsimulations_amd import problem as pb
+    eps = float(np.finfo(float).eps)
+    hnorm = max(max(abs(a) for a in pb.spectral_bounds(p)) for p in probs)
+    out = {"engine": "dense" if dense else "chebyshev", "t_final_s": float(t_final), "hnorm_bound": hnorm,
+           "north_star": 1e-8}
+    if dense:
+        out.update({"value": 1e-10 + 1.5 * eps * hnorm * t_final, "formula": "1e-10 + 1.5 eps ||H|| t"})
+        if os.path.exists(DENSE_GROWTH_N14):
+            with open(DENSE_GROWTH_N14) as f:
+                g = json.load(f)
+            out["measured_n14"] = {"rate_per_s": g["rate_envelope_per_s"], "at_t_final": g["rate_envelope_per_s"] * t_final,
+                                   "source": os.path.relpath(DENSE_GROWTH_N14, ROOT)}
+    else:
+        out.update({"value": 1e-14 * intervals, "formula": "1e-14 per interval x intervals"})
     return out
 
 

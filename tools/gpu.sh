@@ -34,14 +34,15 @@ for T in "$@"; do
       sel=(tests); [ -n "$arg" ] && sel=("$arg")
       [[ "$arg" == k=* ]] && sel=(tests -k "${arg#k=}")
       log=$OUT/gpu_tests${arg:+_$(basename "${arg#k=}" .py)}.log
-      timeout -k 10 1100 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu "${sel[@]}" > $log 2>&1; rc=$?
+      DSE_TEST_RECORD=$OUT timeout -k 10 1100 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu "${sel[@]}" > $log 2>&1; rc=$?
       tail -3 $log; [ $rc -eq 0 ] || fail tests ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
       cat $OUT/smoke.log; [ $rc -eq 0 ] || fail smoke ;;
     bench)
-      timeout -k 10 900 python -u bench.py "${A[@]}" > $OUT/bench.json 2> $OUT/bench.err; rc=$?
-      head -c 600 $OUT/bench.json; echo; [ $rc -eq 0 ] || { tail -5 $OUT/bench.err; fail bench; } ;;
+      nb=$((nb + 1)); b=$OUT/bench$([ $nb -gt 1 ] && echo _$nb)
+      timeout -k 10 900 python -u bench.py "${A[@]}" > $b.json 2> $b.err; rc=$?
+      head -c 600 $b.json; echo; [ $rc -eq 0 ] || { tail -5 $b.err; fail bench; } ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py $LEGS "${A[@]}" > $OUT/bench_under_rocprof.json 2> $OUT/trace.err; rc=$?
       [ $rc -eq 0 ] || fail trace ;;

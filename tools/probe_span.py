@@ -2,7 +2,7 @@
 """Spanning-register timings (dse_span.hip): JSON lines of wall and kernel time.
 
     python3 tools/probe_span.py lone [reps]     one N = 14 register per evolve (center_on and
-                                                shell_off at 75 / 150 kHz), default / span_tile 11 / 10
+                                                shell_off at 75 / 150 kHz), whole / span_tile 11 / 10
     python3 tools/probe_span.py sweep [reps]    the bench's 192 evolutions with default / span_tile 11 / 10
     python3 tools/probe_span.py shard [reps]    one GPU's share of the 64-point sweep on 8 GPUs
                                                 (8 points = 24 evolutions), default / span_tile 11 / 10
@@ -25,10 +25,17 @@ T = np.linspace(0.0, 1e-3, 101)
 
 
 def setting(span):
-    """'0' default kernel, 'tL' option span_tile L, 'sS' option span S"""
-    if span in ("0", 0):
-        return {}
-    return {"span_tile" if span[0] == "t" else "span": int(span[1:])}
+    """'+'-joined tokens: '0' whole registers (span_tile 0), 'a' the automatic policy (default),
+    'tL' option span_tile L, 'sS' option span S, 'rX' option real X (e.g. '0+r0': k_interval)"""
+    opts = {}
+    for tok in str(span).split("+"):
+        if tok == "0":
+            opts["span_tile"] = 0
+        elif tok == "a":
+            opts["span_tile"] = -1
+        else:
+            opts[{"t": "span_tile", "s": "span", "r": "real"}[tok[0]]] = int(tok[1:])
+    return opts
 
 
 def run(eng, probs, span, reps, label, **opts):
@@ -47,7 +54,8 @@ def run(eng, probs, span, reps, label, **opts):
         walls.append((time.perf_counter() - t0) * 1e3)
         kms.append(st["step_kernel_ms"])
     eng.set_option("span", 0)
-    eng.set_option("span_tile", 0)
+    eng.set_option("span_tile", -1)
+    eng.set_option("real", 1)
     eng.clear()
     terms = st["h_applications"]
     rec = {"case": label, "span": span, "n_probs": len(probs), "wall_ms": min(walls),
@@ -56,7 +64,7 @@ def run(eng, probs, span, reps, label, **opts):
            "launches": st["step_launches"], "h_applications": terms,
            "us_per_term_chain": 1e3 * min(kms) / max(1, st["max_degree"] * st["n_intervals"] /
                                                       max(1, st["outputs_per_launch"])),
-           "fallbacks": st["handoff_fallbacks"], **opts}
+           "fallbacks": st["handoff_fallbacks"], "real_problems": st["real_problems"], **opts}
     print(json.dumps(rec), flush=True)
     return obs
 
