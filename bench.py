@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--mixed-launch", type=int, default=int(os.environ.get("DSE_MIXED_LAUNCH", "1")),
                     help="persistent mode: 1- and 2-tile problems in one launch per interval (1, default) "
                     "or one stream each (0)")
-    ap.add_argument("--real", type=int, default=int(os.environ.get("DSE_REAL", "1")),
+    ap.add_argument("--real", type=int, default=int(os.environ.get("DSE_REAL", "0")),
                     help="real-component mode (dse_real.hip) for the 13/14-qubit registers (0: k_interval)")
     ap.add_argument("--obs-overlap", type=int, default=int(os.environ.get("DSE_OBS_OVERLAP", "0")),
                     help="persistent mode: observables on a second stream per lane (1)")

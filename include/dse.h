@@ -185,10 +185,12 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         (default), 2 whenever eligible
  *          "symv_fused"   propagator-matrix mode: 1 sums each product's partials inside the
  *                         product's launch (agent-scope counters); 0 (default) a second launch
- *          "real"         1 (default): registers of 13 / 14 qubits whose drives are all imaginary
+ *          "real"         1: registers of 13 / 14 qubits whose drives are all imaginary
  *                         (the sweep's phase pi/2) run in the rotated frame, where H is real: two
  *                         real Chebyshev recurrences, one workgroup each holding the whole
- *                         register in LDS (k_real, dse_real.hip); 0: the complex kernels
+ *                         register in LDS (k_real, dse_real.hip); 0 (default): the complex
+ *                         kernels (k_real measured at the 2-tile k_interval's CU cost, slower on
+ *                         the bench's mix of 13- and 14-qubit registers)
  *          "span_tile"    L > 0 (10 or 11): every register of n > L qubits runs over 2^(n - L)
  *                         cooperating workgroups, one per CU, with per-term cross-tile hand-offs
  *                         (k_span, dse_span.hip): a shorter chain per register for few registers

@@ -160,6 +160,7 @@ hipError_t launch_span(int L, int RB, bool imag, const DevProb* probs, const Spa
 bool span_supported(int L, int RB);
 hipError_t set_span_spin_limit(int limit);
 hipError_t set_span_ablate(int mask);
+hipError_t set_real_ablate(int mask);
 hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu);
 
 // ---- real-component registers (dse_real.hip) ------------------------------------------------

@@ -87,7 +87,12 @@ __device__ __forceinline__ void rd_pairs(uint32_t wbase, int tp, int hh, int pp0
   }
 }
 
-template <int L>
+// diagnostics only (option real_ablate, separate instantiations; results become wrong): 1 phase 1,
+// 2 the sweeps' FMAs, 4 the thread pairs, 8 the propagator sums' global loads and stores, 16 the
+// w_k stores
+int g_real_ablate = 0;
+
+template <int L, int ABL>
 __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int comp, int set, int n_out) {
   constexpr int NT = kRealNT, TB = kRealTB, RB = L - TB, R = 1 << RB, RP = R / 2, HRP = RP / 2;
   constexpr int RH = R / 2;  // rows per half
@@ -161,6 +166,7 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
   for (int r = 0; r < R; ++r) prev[r] = 0.0;
   const uint32_t wb = lds_u32(&S.w[0]);
   const int rfm = ctab->rflip_mask;
+  constexpr int ab = ABL;
 
   for (int k = 1; k <= K; ++k) {
     // ---- phase 1: diagonal, drives and pairs among register bits (own rows), one half of the
@@ -222,10 +228,15 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
           }
         }
       };
-      own_half(0);
-      own_half(1);
-      cross_half(0);
-      cross_half(1);
+      if constexpr (!(ab & 1)) {
+        own_half(0);
+        own_half(1);
+        cross_half(0);
+        cross_half(1);
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) out[r] = 0.0;
+      }
     }
     __syncthreads();  // (first term: the setup's stores; later: w_{k-1} complete in LDS)
 
@@ -279,6 +290,22 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
       };
       constexpr int QP = HRP / 2;  // row pairs per quarter
       double qa[2 * QP], qb[2 * QP];
+      if constexpr ((ab & 6) != 0) {  // ablation variants (diagnostics)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          if (hh) rd_pairs<HRP, HRP>(wb, pt, 1, 0, pv);
+          if (!(ab & 2)) sweep(hh, pv);
+          if (!(ab & 4))
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+              rd_pairs<HRP, HRP>(wb, tpt[qq], hh, 0, qa);
+              double* oh = out + hh * RH;
+#pragma unroll
+              for (int rr = 0; rr < 2 * QP; ++rr) oh[rr] = fma(ge[qq], qa[rr], oh[rr]);
+            }
+        }
+        continue;
+      }
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         rd_pairs<HRP, QP>(wb, tpt[0], hh, 0, qa);
@@ -304,59 +331,81 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
       }
     }
 
-    // ---- phase 5: recurrence, complex propagator sums (every third term), w_k -> LDS ----
+    // ---- phase 5: recurrence, complex propagator sums (every third term), w_k -> LDS.  The sums'
+    // global loads run D blocks ahead of their use (the compiler cannot hoist them above the
+    // previous blocks' stores to the same arrays), so their latency is exposed once per update ----
 #pragma unroll
     for (int r = 0; r < R; ++r) out[r] = k == 1 ? s1 * out[r] : fma(2.0 * s1, out[r], -prev[r]);
-    bool upd[kMaxOut];
+    static_assert(kMaxOut == 2, "phase 5 dispatch covers one or two outputs per launch");
+    int um = 0;
     double2* accp[kMaxOut];
+    CoefK cf[kMaxOut];  // a_{k-2}, a_{k-1}, a_k of each output (zero when it does not update)
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
-      upd[j] = j < n_out && coef_nterm(k, dj[j]) > 0;
+      cf[j] = j < n_out ? coef_at(coef_row(P, set, j), k) : CoefK{};
+      um |= cf[j].upd ? 1 << j : 0;
       accp[j] = P.racc + ((size_t)(2 * j + comp) << L);
     }
+    // NO outputs of the launch; a term where some output updates loads and stores all NO sums
+    // (an output past its degree has zero coefficients: its sums pass through unchanged)
+    auto phase5 = [&](auto no_c) {
+      constexpr int NO = decltype(no_c)::value;
+      constexpr bool ACC = NO > 0 && !(ab & 8);
+      constexpr int NB = R / AB, D = 3;
+      const bool first = k == 1;
+      double2 av[D][kMaxOut][AB];
+      auto issue = [&](int b, int slot) {
 #pragma unroll
-    for (int r0 = 0; r0 < R; r0 += AB) {
-      double ownb[AB];
+        for (int j = 0; j < NO; ++j)
 #pragma unroll
-      for (int r = 0; r < AB; r += 2) {
-        const dv2 d = S.w[((r0 + r) >> 1) * NT + tid];
-        ownb[r] = d.x;
-        ownb[r + 1] = d.y;
+          for (int r = 0; r < AB; ++r) av[slot][j][r] = gld(gptr(accp[j]), (size_t)(b * AB + r) * NT + tid);
+      };
+      if constexpr (ACC) {
+#pragma unroll
+        for (int b = 0; b < D; ++b) issue(b, b);
       }
-      double2 accv[kMaxOut][AB];
 #pragma unroll
-      for (int j = 0; j < kMaxOut; ++j)
-        if (upd[j] && k > 1) {
+      for (int b = 0; b < NB; ++b) {
+        double ownb[AB];
 #pragma unroll
-          for (int r = 0; r < AB; ++r) accv[j][r] = gld(gptr(accp[j]), (size_t)(r0 + r) * NT + tid);
+        for (int r = 0; r < AB; r += 2) {
+          const dv2 d = S.w[((b * AB + r) >> 1) * NT + tid];
+          ownb[r] = d.x;
+          ownb[r + 1] = d.y;
         }
+        if constexpr (NO > 0) {
 #pragma unroll
-      for (int j = 0; j < kMaxOut; ++j) {
-        if (!upd[j]) continue;
-        const int nt = coef_nterm(k, dj[j]);
-        const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);  // a_{k-2}, a_{k-1}, a_k
-        const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
-                      c1 = nt >= 2 ? make_double2(cc[2], cc[3]) : make_double2(0.0, 0.0),
-                      c2 = make_double2(cc[4], cc[5]);
+          for (int j = 0; j < NO; ++j)
 #pragma unroll
-        for (int r = 0; r < AB; ++r) {
-          double2 a = make_double2(0.0, 0.0);
-          if (k > 1) {
-            a = accv[j][r];
-            a.x = fma(c0.x, prev[r0 + r], a.x);
-            a.y = fma(c0.y, prev[r0 + r], a.y);
+            for (int r = 0; r < AB; ++r) {
+              double2 a = make_double2(0.0, 0.0);
+              if constexpr (ACC) {
+                a = first ? make_double2(0.0, 0.0) : av[b % D][j][r];
+                a.x = fma(cf[j].c[0].x, prev[b * AB + r], a.x);
+                a.y = fma(cf[j].c[0].y, prev[b * AB + r], a.y);
+              }
+              a.x = fma(cf[j].c[1].x, ownb[r], a.x);
+              a.y = fma(cf[j].c[1].y, ownb[r], a.y);
+              a.x = fma(cf[j].c[2].x, out[b * AB + r], a.x);
+              a.y = fma(cf[j].c[2].y, out[b * AB + r], a.y);
+              if constexpr (ACC) gst(gptr(accp[j]), (size_t)(b * AB + r) * NT + tid, a);
+            }
+          if constexpr (ACC) {
+            if (b + D < NB) issue(b + D, b % D);
           }
-          a.x = fma(c1.x, ownb[r], a.x);
-          a.y = fma(c1.y, ownb[r], a.y);
-          a.x = fma(c2.x, out[r0 + r], a.x);
-          a.y = fma(c2.y, out[r0 + r], a.y);
-          gst(gptr(accp[j]), (size_t)(r0 + r) * NT + tid, a);
         }
-      }
 #pragma unroll
-      for (int r = 0; r < AB; ++r) prev[r0 + r] = ownb[r];
-    }
+        for (int r = 0; r < AB; ++r) prev[b * AB + r] = ownb[r];
+      }
+    };
+    if (um == 0)
+      phase5(std::integral_constant<int, 0>());
+    else if (n_out >= 2)
+      phase5(std::integral_constant<int, 2>());
+    else
+      phase5(std::integral_constant<int, 1>());
     __syncthreads();  // every read of w_{k-1} done
+    if (!(ab & 16))
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
       dv2 d;
@@ -367,15 +416,16 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
   }
 }
 
+template <int ABL>
 __global__ void __launch_bounds__(kRealNT)
 k_real(const DevProb* __restrict__ probs, const int2* __restrict__ items, int set, int n_out) {
   __shared__ RealShared S;
   const int2 it = items[blockIdx.x];
   const DevProb& P = probs[it.x];
   if (P.n == 14)
-    real_body<14>(S, P, it.y, set, n_out);
+    real_body<14, ABL>(S, P, it.y, set, n_out);
   else
-    real_body<13>(S, P, it.y, set, n_out);
+    real_body<13, ABL>(S, P, it.y, set, n_out);
 }
 
 // psi_j = i^{|x0| - |x|} (acc_a + i acc_b) of output j into the buffer k_obs reads (the last output:
@@ -416,14 +466,30 @@ k_real_init(const DevProb* __restrict__ probs, const int2* __restrict__ items) {
 
 }  // namespace
 
+hipError_t set_real_ablate(int mask) {
+  if (mask != 0 && mask != 1 && mask != 2 && mask != 4 && mask != 6 && mask != 8 && mask != 16)
+    return hipErrorInvalidValue;
+  g_real_ablate = mask;
+  return hipSuccess;
+}
+
 hipError_t real_occupancy(int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_real, kRealNT, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_real<0>, kRealNT, 0);
 }
 
 hipError_t launch_real(const DevProb* probs, const int2* items, int n_items, int set, int n_out,
                        hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_real, dim3(n_items), dim3(kRealNT), 0, st, probs, items, set, n_out);
+  const dim3 g(n_items), b(kRealNT);
+  switch (g_real_ablate) {
+    case 1: hipLaunchKernelGGL(k_real<1>, g, b, 0, st, probs, items, set, n_out); break;
+    case 2: hipLaunchKernelGGL(k_real<2>, g, b, 0, st, probs, items, set, n_out); break;
+    case 4: hipLaunchKernelGGL(k_real<4>, g, b, 0, st, probs, items, set, n_out); break;
+    case 6: hipLaunchKernelGGL(k_real<6>, g, b, 0, st, probs, items, set, n_out); break;
+    case 8: hipLaunchKernelGGL(k_real<8>, g, b, 0, st, probs, items, set, n_out); break;
+    case 16: hipLaunchKernelGGL(k_real<16>, g, b, 0, st, probs, items, set, n_out); break;
+    default: hipLaunchKernelGGL(k_real<0>, g, b, 0, st, probs, items, set, n_out);
+  }
   return hipGetLastError();
 }
 

@@ -240,9 +240,9 @@ struct dse_ctx {
   int span = 0;
   int span_tile = -1;               // option "span_tile": L > 0 every register of n > L qubits spans 2^(n-L)
                                     // tiles; -1 (default) auto: L = 11 when all tiles fit the chip at once
-  // real-component mode (dse_real.hip, option "real", default 1): registers of 13 or 14 qubits with
+  // real-component mode (dse_real.hip, option "real", default 0): registers of 13 or 14 qubits with
   // imaginary drives run as two real recurrences, one workgroup per component, no hand-off
-  int real_mode = 1;
+  int real_mode = 0;
   unsigned char* d_real = nullptr;  // [a | b] inputs and propagator sums of the real-mode registers
   size_t real_cap = 0;
   unsigned char* d_real_tab = nullptr;
@@ -1397,6 +1397,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "ablate") {  // diagnostics only: skip kernel sections (results become wrong)
     HIPC(set_ablate((int)value));
     HIPC(set_ablate_interval((int)value));
+  } else if (k == "real_ablate") {  // diagnostics only: skip k_real sections (results become wrong)
+    HIPC(set_real_ablate((int)value));
   } else if (k == "span_ablate") {  // diagnostics only: skip k_span sections (results become wrong)
     HIPC(set_span_ablate((int)value));
   } else if (k == "probe_items") {  // diagnostics only: dse_time_step_kernel launches this many items

@@ -69,7 +69,7 @@ def test_production_interval_kernel_matches_reference_n14(engine, golden, m, rea
     assert all(np.count_nonzero(p.pair[:13, 13]) == 13 for p in probs[6:])  # shell_off: 13 pairs cross
     engine.clear()
     engine.set_option("outputs_per_launch", m)
-    engine.set_option("real", real)   # 1 (default): k_real, two real recurrences; 0: k_interval
+    engine.set_option("real", real)   # 1: k_real, two real recurrences; 0 (default): k_interval
     engine.set_option("span_tile", 0)  # whole registers (no automatic span)
     try:
         for p in probs:
@@ -77,7 +77,7 @@ def test_production_interval_kernel_matches_reference_n14(engine, golden, m, rea
         obs, st = engine.evolve(t)
     finally:
         engine.set_option("outputs_per_launch", 2)
-        engine.set_option("real", 1)
+        engine.set_option("real", 0)
         engine.set_option("span_tile", -1)
         engine.clear()
     assert st["mode"] == 1 and st["tile_bits"] == 13 and st["outputs_per_launch"] == m
@@ -159,7 +159,7 @@ def test_mixed_launch_is_bitwise_identical(engine):
             obs, st = engine.evolve(t)
         finally:
             engine.set_option("mixed_launch", 1)
-            engine.set_option("real", 1)
+            engine.set_option("real", 0)
             engine.set_option("span_tile", -1)
             engine.clear()
         assert st["mode"] == 1
@@ -191,7 +191,7 @@ def test_overlapped_observables_are_bitwise_identical(engine, m):
         finally:
             engine.set_option("obs_overlap", 0)
             engine.set_option("outputs_per_launch", 2)
-            engine.set_option("real", 1)
+            engine.set_option("real", 0)
             engine.set_option("span_tile", -1)
             engine.clear()
         assert st["mode"] == 1 and st["outputs_per_launch"] == m

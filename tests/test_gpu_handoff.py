@@ -21,12 +21,12 @@ T = np.linspace(0.0, 2e-5, 5)
 
 @pytest.fixture(autouse=True)
 def _interval_kernel(engine):
-    """These tests exercise k_interval's 2-tile hand-off: the real-component mode (dse_real.hip,
-    default for these registers, no hand-off at all) is switched off for them."""
+    """These tests exercise k_interval's 2-tile hand-off: the real-component mode (dse_real.hip, no
+    hand-off at all) and the automatic span are switched off for them."""
     engine.set_option("real", 0)
     engine.set_option("span_tile", 0)  # whole registers (no automatic span)
     yield
-    engine.set_option("real", 1)
+    engine.set_option("real", 0)
     engine.set_option("span_tile", -1)
 
 

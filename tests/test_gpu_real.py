@@ -37,7 +37,7 @@ def _run(engine, probs, real, m=2):
         states = [engine.state(i) for i in range(len(probs))]
         energies = [engine.energy(i) for i in range(len(probs))]
     finally:
-        engine.set_option("real", 1)
+        engine.set_option("real", 0)
         engine.set_option("span_tile", -1)
         engine.set_option("outputs_per_launch", 2)
         engine.clear()

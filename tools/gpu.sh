@@ -52,12 +52,12 @@ for T in "$@"; do
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- python3 bench.py $LEGS --steps 1 --warmup 0 > $OUT/write.json 2> $OUT/write.err; rc=$?
       [ $rc -eq 0 ] || fail write ;;
     sq)
-      PMC_CMD=(python3 tools/probe_one.py "${A[@]}")
-      pmc p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU; rc=$?
+      PMC_CMD=(python3 tools/probe_one.py "${A[@]}"); q=$(echo "${A[*]}" | tr ' =' '__')_
+      pmc ${q}p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU; rc=$?
       [ $rc -eq 0 ] || fail sq p1
-      pmc p2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE; rc=$?
+      pmc ${q}p2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE; rc=$?
       [ $rc -eq 0 ] || fail sq p2
-      pmc p3 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE; rc=$?
+      pmc ${q}p3 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE; rc=$?
       [ $rc -eq 0 ] || fail sq p3 ;;
     sytrd)
       for n in "${A[@]}"; do

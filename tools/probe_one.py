@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Diagnostic driver for counter collection: one output interval of the N = 14 sweep set
-("singles" = center_off 1-tile problems, "pairs" = 2-tile problems, "all"), evolved 3 times.
+("singles" = center_off 1-tile problems, "pairs" = 2-tile problems, "all"), evolved 3 times,
+with engine options given as k=v (e.g. real=0,span_tile=0 for k_interval; the defaults pick k_real
+or k_span).
 
-    rocprofv3 --pmc SQ_WAVES ... -- python3 tools/probe_one.py singles
+    rocprofv3 --pmc SQ_WAVES ... -- python3 tools/probe_one.py singles real=0,span_tile=0
 """
 import os
 import sys
@@ -23,12 +25,16 @@ def main():
     t = np.linspace(0.0, 1e-5, 2)
     with Engine(0, tile_bits=13) as eng:
         eng.set_option("streams", 1)
+        for kv in ",".join(sys.argv[2:]).split(",") if len(sys.argv) > 2 else []:
+            k, v = kv.split("=")
+            eng.set_option(k, float(v))
         for p in probs:
             if which == "all" or (which == "pairs") == (p.n_qubits == 14):
                 eng.add(p)
         for _ in range(3):
             _, st = eng.evolve(t)
-        print(which, st["max_degree"], st["step_kernel_ms"] / max(st["timed_launches"], 1), flush=True)
+        print(which, st["max_degree"], st["step_kernel_ms"] / max(st["timed_launches"], 1),
+              "real", st["real_problems"], "span", st["span_problems"], flush=True)
 
 
 if __name__ == "__main__":

@@ -55,7 +55,7 @@ def run(eng, probs, span, reps, label, **opts):
         kms.append(st["step_kernel_ms"])
     eng.set_option("span", 0)
     eng.set_option("span_tile", -1)
-    eng.set_option("real", 1)
+    eng.set_option("real", 0)
     eng.clear()
     terms = st["h_applications"]
     rec = {"case": label, "span": span, "n_probs": len(probs), "wall_ms": min(walls),
@@ -86,6 +86,12 @@ def main():
                         else:
                             print(json.dumps({"check": f"{variant}_{int(d / 1e3)}k", "span": s,
                                               "max_abs_diff_vs_span0": float(np.max(np.abs(obs - ref)))}), flush=True)
+        elif what == "rablate":  # probe_span.py rablate <reps> - <mask/...>: k_real sections off (lone N=14)
+            p = pb.build_problem(sweep_point_params(13, 150e3, "shell_off", T[-1], len(T)))
+            masks = [int(m) for m in (sys.argv[4].split("/") if len(sys.argv) > 4 else ["0"])]
+            for m in masks:
+                run(eng, [p], "0", reps, f"shell_off_150k_real_ablate{m}", real_ablate=m)
+            eng.set_option("real_ablate", 0)
         elif what == "ablate":  # probe_span.py ablate <reps> <setting> <mask/mask/...>: k_span sections off
             p = pb.build_problem(sweep_point_params(13, 150e3, "center_on", T[-1], len(T)))
             masks = [int(m) for m in (sys.argv[4].split("/") if len(sys.argv) > 4 else ["0"])]
