@@ -1379,7 +1379,8 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     if (!(value >= 0 && value <= kSpanMaxTop)) return fail(ctx, DSE_ERR_ARG, "span must be in 0..4");
     ctx->span = (int)value;
   } else if (k == "real") {  // real-component mode for registers of 13 / 14 qubits (imaginary drives)
-    ctx->real_mode = value != 0.0;
+    if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "real must be 0, 1 or 2");
+    ctx->real_mode = (int)value;
   } else if (k == "span_tile") {  // spanning registers: tile bits L (0 off, -1 auto); n > L qubits span 2^(n-L) tiles
     if (!(value == 0 || value == -1 || (value >= 10 && value <= 13)))
       return fail(ctx, DSE_ERR_ARG, "span_tile must be -1, 0 or in 10..13");
@@ -2720,16 +2721,20 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   }
   if (!persistent)
     for (auto& P : ctx->probs) P.span_s = 0;
-  // real-component mode: when every Chebyshev register qualifies (one launch kind per interval)
+  // real-component mode: option real = 1 when every Chebyshev register qualifies (one launch kind
+  // per interval); real = 2 the 2-tile (14-qubit) registers only, on their own stream beside the
+  // 1-tile registers' k_interval launches (neither kernel waits on another workgroup, so the two
+  // persistent launches share the chip without a residency condition)
   {
     bool real_mode = persistent && ctx->real_mode && !ctx->obs_overlap;
     int n_cheb = 0;
     for (auto& P : ctx->probs) {
       if (P.side()) continue;
       ++n_cheb;
-      real_mode = real_mode && real_eligible(P);
+      if (ctx->real_mode == 1) real_mode = real_mode && real_eligible(P);
     }
-    for (auto& P : ctx->probs) P.rl = real_mode && n_cheb > 0 && !P.side();
+    for (auto& P : ctx->probs)
+      P.rl = real_mode && n_cheb > 0 && !P.side() && (ctx->real_mode == 1 || (real_eligible(P) && P.n_tiles == 2));
   }
   // streaming: registers of more than one 2^13 tile take the Walsh-Hadamard engine (option wht)
   bool used_wht = false;
@@ -3040,10 +3045,11 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // pair whose partner is still queued waits only for a workgroup that needs no partner.
   std::map<int, std::pair<int64_t, int64_t>> tiles_per_L;  // L -> (1-tile problems, 2-tile problems)
   for (auto& P : ctx->probs)
-    if (!P.side() && !P.span_s && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
+    if (!P.side() && !P.span_s && !P.rl && P.shard_bits == 0 && (P.n_tiles == 1 || P.n_tiles == 2))
       (P.n_tiles == 1 ? tiles_per_L[P.L].first : tiles_per_L[P.L].second) += 1;
   auto mixed_L = [&](const HostProblem& P) {
-    if (!persistent || !ctx->mixed_launch || P.side() || P.span_s || P.shard_bits != 0 || P.n_tiles > 2) return false;
+    if (!persistent || !ctx->mixed_launch || P.side() || P.span_s || P.rl || P.shard_bits != 0 || P.n_tiles > 2)
+      return false;
     const auto it = tiles_per_L.find(P.L);
     return it != tiles_per_L.end() && it->second.first > 0 && it->second.second > 0 &&
            2 * it->second.second <= cap;

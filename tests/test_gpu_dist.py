@@ -64,6 +64,7 @@ def test_partitioned_over_processes_matches_unsharded(engine, n, world, wht):
     v = rng.standard_normal(1 << n) + 1j * rng.standard_normal(1 << n)
     engine.clear()
     engine.set_option("wht", wht)
+    engine.set_option("span_tile", 0)  # the unsharded reference on the same engine family
     try:
         p0 = engine.add(prob)
         hv = engine.apply_h(p0, v)
@@ -72,6 +73,7 @@ def test_partitioned_over_processes_matches_unsharded(engine, n, world, wht):
         s_ref = engine.state(p0)
     finally:
         engine.set_option("wht", 1)
+        engine.set_option("span_tile", -1)
         engine.clear()
     parts = np.split(hv, world)
     sparts = np.split(s_ref, world)

@@ -9,7 +9,9 @@ test_gpu_config3.py (parametrised over the mode).
   64 detunings, 1 ms / 101 outputs, one and two outputs per launch: <O>(t) within 1e-11;
 * the final state in the computational frame (the combine's i^{|x0| - |x|} phases, the shift
   folded into H') equals k_interval's (dse_get_state), and its energy;
-* bitwise repeatable.
+* bitwise repeatable;
+* option real = 2: only the 14-qubit (2-tile) registers on k_real, the 13-qubit ones on the 1-tile
+  k_interval on a second stream at the same time, against real = 0 (1e-11).
 """
 import numpy as np
 import pytest
@@ -65,3 +67,16 @@ def test_real_mode_is_repeatable(engine):
     runs = [_run(engine, probs, 1)[0] for _ in range(3)]
     for r in runs[1:]:
         assert np.array_equal(r, runs[0])
+
+
+def test_mixed_real_and_interval_registers(engine):
+    probs = _probs()
+    ob_m, st_m, s_m, _ = _run(engine, probs, 2)
+    ob_c, st_c, s_c, _ = _run(engine, probs, 0)
+    n14 = sum(1 for p in probs if p.n_qubits == 14)
+    assert 0 < n14 < len(probs) and st_m["real_problems"] == n14 and st_c["real_problems"] == 0
+    err = float(np.max(np.abs(ob_m - ob_c)))
+    print(f"real = 2 vs k_interval: max |d<O>| = {err:.2e}")
+    assert err < 1e-11, err
+    for a, b in zip(s_m, s_c):
+        assert np.max(np.abs(a - b)) < 1e-11

@@ -10,6 +10,7 @@
 #   bench[:args]               python bench.py <args>  (args: comma-separated)
 #   trace                      rocprofv3 --kernel-trace --stats of the bench's sweep leg
 #   traffic                    FETCH_SIZE and WRITE_SIZE passes of the same (one counter per run)
+#   traffic_large              the same over tools/bench_large.py (N = 30, Walsh-Hadamard engine)
 #   sq:<set>                   three SQ counter passes over tools/probe_one.py <set>
 #   sytrd:<dim,...>            tools/bin/probe_sytrd <dim> check
 #   py:<script>,<args...>      python -u <script> <args> > <tag>/<script-name>.out
@@ -51,6 +52,11 @@ for T in "$@"; do
       [ $rc -eq 0 ] || fail fetch
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- python3 bench.py $LEGS --steps 1 --warmup 0 > $OUT/write.json 2> $OUT/write.err; rc=$?
       [ $rc -eq 0 ] || fail write ;;
+    traffic_large)  # FETCH_SIZE / WRITE_SIZE passes over the N = 30 register (tools/bench_large.py)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/large/fetch -o fetch --output-format csv -- python3 tools/bench_large.py --steps 3 > $OUT/large_fetch.json 2> $OUT/large_fetch.err; rc=$?
+      [ $rc -eq 0 ] || fail fetch_large
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/large/write -o write --output-format csv -- python3 tools/bench_large.py --steps 3 > $OUT/large_write.json 2> $OUT/large_write.err; rc=$?
+      [ $rc -eq 0 ] || fail write_large ;;
     sq)
       PMC_CMD=(python3 tools/probe_one.py "${A[@]}"); q=$(echo "${A[*]}" | tr ' =' '__')_
       pmc ${q}p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU; rc=$?

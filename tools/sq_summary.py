@@ -7,18 +7,21 @@
 Counters are summed over the dispatches of a kernel, then divided by the dispatch count.
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles summed over waves
 (MI355X_MICROARCH.md, PMC table); WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES.
-GRBM_GUI_ACTIVE is the dispatch's duration in GPU cycles.  Derived (per wave, then per SIMD):
+GRBM_GUI_ACTIVE is summed over the 8 XCDs: / 8 = the dispatch's duration in cycles (checked
+against the HIP-event time of the same launches at ~2.1 GHz).  Derived (per wave, then per SIMD):
   issue_frac         ACTIVE_INST_ANY / WAVE_CYCLES   (a wave's life spent issuing)
   wait_frac          WAIT_ANY / WAVE_CYCLES          (parked on s_waitcnt / barrier)
   stall_frac         WAIT_INST_ANY / WAVE_CYCLES     (issue stalls: dependency, pipe busy)
   lds_stall_frac     WAIT_INST_LDS / WAVE_CYCLES
   valu_frac          ACTIVE_INST_VALU / WAVE_CYCLES
-  waves_per_simd     4 WAVE_CYCLES / (GRBM_GUI_ACTIVE x SIMDs holding the kernel's workgroups)
-  valu_busy          valu_frac x waves_per_simd     (fraction of SIMD cycles issuing VALU)
-  lds_busy           SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE x CUs in use)  (LDS-array cycles per CU cycle)
+  cycles             GRBM_GUI_ACTIVE / 8
+  waves_per_simd_counter  4 WAVE_CYCLES / (cycles x SIMDs holding the kernel's workgroups) (reads
+                     ~0.7 x the resident waves for persistent kernels: a counter-unit caveat, use
+                     the launch configuration for occupancy)
+  fp64_busy          4 cycles x (FMA_F64 + ADD_F64 + MUL_F64) / (4 SIMDs x CUs in use x cycles)
+  lds_busy           SQ_LDS_IDX_ACTIVE / (CUs in use x cycles)  (LDS-array cycles per CU cycle)
   lds_conflict_frac  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   fp64_flop          64 x (2 FMA_F64 + ADD_F64 + MUL_F64) per dispatch (all lanes active assumed)
-  fp64_frac_of_cu_peak  fp64_flop / (GRBM_GUI_ACTIVE x CUs in use x 128 flop/clk)
 """
 import collections
 import csv
@@ -59,34 +62,34 @@ def main():
         d = {"dispatches": max(len(v) for v in cs.values()), "workgroups": wgs, **m, "counters": c}
         wc = c.get("SQ_WAVE_CYCLES")
         gui = c.get("GRBM_GUI_ACTIVE")
+        cyc = gui / 8.0 if gui else None
+        if cyc:
+            d["cycles"] = cyc
         if wc:
             for key, num in (("issue_frac", "SQ_ACTIVE_INST_ANY"), ("wait_frac", "SQ_WAIT_ANY"),
                              ("stall_frac", "SQ_WAIT_INST_ANY"), ("lds_stall_frac", "SQ_WAIT_INST_LDS"),
                              ("valu_frac", "SQ_ACTIVE_INST_VALU")):
                 if num in c:
                     d[key] = c[num] / wc
-        if wc and gui:
-            d["waves_per_simd"] = 4.0 * wc / (gui * simds)
-            if "valu_frac" in d:
-                d["valu_busy"] = d["valu_frac"] * d["waves_per_simd"]
-        if gui and "SQ_LDS_IDX_ACTIVE" in c:
-            d["lds_busy"] = c["SQ_LDS_IDX_ACTIVE"] / (gui * cus)
+        if wc and cyc:
+            d["waves_per_simd_counter"] = 4.0 * wc / (cyc * simds)
+        if cyc and "SQ_LDS_IDX_ACTIVE" in c:
+            d["lds_busy"] = c["SQ_LDS_IDX_ACTIVE"] / (cus * cyc)
         if c.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"]
         if "SQ_INSTS_VALU_FMA_F64" in c:
-            fl = 64.0 * (2 * c["SQ_INSTS_VALU_FMA_F64"] + c.get("SQ_INSTS_VALU_ADD_F64", 0.0) +
-                         c.get("SQ_INSTS_VALU_MUL_F64", 0.0))
-            d["fp64_flop"] = fl
-            if gui:
-                d["fp64_frac_of_cu_peak"] = fl / (gui * cus * 128.0)
+            n64 = c["SQ_INSTS_VALU_FMA_F64"] + c.get("SQ_INSTS_VALU_ADD_F64", 0.0) + c.get("SQ_INSTS_VALU_MUL_F64", 0.0)
+            d["fp64_flop"] = 64.0 * (n64 + c["SQ_INSTS_VALU_FMA_F64"])
+            if cyc:
+                d["fp64_busy"] = 4.0 * n64 / (4.0 * cus * cyc)
         res[k] = d
     rec = {"source": f"rocprofv3 --pmc, three SQ passes over tools/probe_one.py ({prefix.rstrip('_')})",
            "definitions": __doc__.split("Derived")[1].strip(), "kernels": res}
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
-    for k, d in sorted(res.items(), key=lambda kv: -kv[1]["counters"].get("GRBM_GUI_ACTIVE", 0)):
-        print(k, {x: round(d[x], 3) for x in ("waves_per_simd", "issue_frac", "valu_busy", "lds_busy",
-                                            "lds_conflict_frac", "fp64_frac_of_cu_peak") if x in d})
+    for k, d in sorted(res.items(), key=lambda kv: -kv[1]["counters"].get("GRBM_GUI_ACTIVE", 0))[:3]:
+        print(k, {x: round(d[x], 3) for x in ("waves_per_simd_counter", "issue_frac", "wait_frac", "stall_frac",
+                                            "fp64_busy", "lds_busy", "lds_conflict_frac") if x in d})
 
 
 if __name__ == "__main__":
