@@ -52,6 +52,14 @@ __device__ __forceinline__ void gst(gd2* p, size_t i, double2 a) {
   p[i] = v;
 }
 
+// A wave-uniform double moved into SGPRs (a vector load of a uniform address leaves it in VGPRs)
+__device__ __forceinline__ double uniform_d(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 // Buffer-resource views of one tile (wave-uniform base, 32-bit byte offsets): per-register
 // accesses become buffer ops with the register offset in an SGPR instead of one 64-bit VGPR
 // address per register.  aux = kSc1 makes a store write-through to the coherence point and a load

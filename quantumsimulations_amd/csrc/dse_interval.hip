@@ -587,63 +587,47 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       }
     }
     constexpr int AB = kMaxOut <= 2 ? 4 : (kMaxOut == 3 ? 2 : 1);  // VGPR budget: AB x kMaxOut loads
-    static_assert(kMaxOut == 2, "phase 5 dispatch covers one or two outputs per launch");
     const int nj = (ab & 256) ? 0 : n_out;
-    int um = 0;
-    CoefK cf[kMaxOut];  // a_{k-2}, a_{k-1}, a_k of each output (zero when it does not update)
+    bool upd[kMaxOut];
     __amdgpu_buffer_rsrc_t acc_j[kMaxOut];
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
-      cf[j] = j < nj ? coef_at(coef_row(P, set, j), k) : CoefK{};
-      um |= cf[j].upd ? 1 << j : 0;
+      upd[j] = j < nj && coef_nterm(k, dj[j]) > 0;
       acc_j[j] = (j == n_out - 1) ? acc_t
                                   : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << (L + P.tbl)) + (h << L), TBYTES);
     }
-    // NO outputs: a term where some output updates loads and stores the sums of all NO (one past
-    // its degree has zero coefficients and passes through unchanged); the loads run D blocks ahead
-    // of their use, so their latency is exposed once per update, not once per block
-    auto phase5 = [&](auto no_c) {
-      constexpr int NO = decltype(no_c)::value;
-      constexpr int NB = R / AB, D = NB >= 2 ? 2 : 1;
-      const bool first = k == 1;
-      double2 av[D][kMaxOut][AB];
-      auto issue = [&](int b, int slot) {
 #pragma unroll
-        for (int j = 0; j < NO; ++j)
+    for (int r0 = 0; r0 < R; r0 += AB) {
+      double2 ownb[AB];
 #pragma unroll
-          for (int r = 0; r < AB; ++r) av[slot][j][r] = bld(acc_j[j], voff, (uint32_t)((b * AB + r) * NT * 16));
-      };
-      if constexpr (NO > 0) {
+      for (int r = 0; r < AB; ++r) ownb[r] = S.w[(r0 + r) * NT + tid];
+      double2 accv[kMaxOut][AB];
 #pragma unroll
-        for (int b = 0; b < D; ++b) issue(b, b);
-      }
+      for (int j = 0; j < kMaxOut; ++j)
+        if (upd[j] && k > 1) {
 #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        double2 ownb[AB];
-#pragma unroll
-        for (int r = 0; r < AB; ++r) ownb[r] = S.w[(b * AB + r) * NT + tid];
-        if constexpr (NO > 0) {
-#pragma unroll
-          for (int j = 0; j < NO; ++j)
-#pragma unroll
-            for (int r = 0; r < AB; ++r) {
-              double2 a = first ? make_double2(0.0, 0.0) : cmad(av[b % D][j][r], cf[j].c[0].x, cf[j].c[0].y, prev[b * AB + r]);
-              a = cmad(a, cf[j].c[1].x, cf[j].c[1].y, ownb[r]);
-              a = cmad(a, cf[j].c[2].x, cf[j].c[2].y, out[b * AB + r]);
-              bst(acc_j[j], voff, (uint32_t)((b * AB + r) * NT * 16), a);
-            }
-          if (b + D < NB) issue(b + D, b % D);
+          for (int r = 0; r < AB; ++r) accv[j][r] = bld(acc_j[j], voff, (uint32_t)((r0 + r) * NT * 16));
         }
 #pragma unroll
-        for (int r = 0; r < AB; ++r) prev[b * AB + r] = ownb[r];
+      for (int j = 0; j < kMaxOut; ++j) {
+        if (!upd[j]) continue;
+        const int nt = coef_nterm(k, dj[j]);
+        const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);  // a_{k-2}, a_{k-1}, a_k
+        const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
+                      c1 = nt >= 2 ? make_double2(cc[2], cc[3]) : make_double2(0.0, 0.0),
+                      c2 = make_double2(cc[4], cc[5]);
+#pragma unroll
+        for (int r = 0; r < AB; ++r) {
+          double2 a = make_double2(0.0, 0.0);
+          if (k > 1) a = cmad(accv[j][r], c0.x, c0.y, prev[r0 + r]);
+          a = cmad(a, c1.x, c1.y, ownb[r]);
+          a = cmad(a, c2.x, c2.y, out[r0 + r]);
+          bst(acc_j[j], voff, (uint32_t)((r0 + r) * NT * 16), a);
+        }
       }
-    };
-    if (um == 0)
-      phase5(std::integral_constant<int, 0>());
-    else if (nj >= 2)
-      phase5(std::integral_constant<int, 2>());
-    else
-      phase5(std::integral_constant<int, 1>());
+#pragma unroll
+      for (int r = 0; r < AB; ++r) prev[r0 + r] = ownb[r];
+    }
     __syncthreads();  // every read of w_{k-1} in LDS is done
     if (s_fail) break;  // uniform: a hand-off timed out (error reported to the host)
 #pragma unroll

@@ -342,7 +342,14 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
     CoefK cf[kMaxOut];  // a_{k-2}, a_{k-1}, a_k of each output (zero when it does not update)
 #pragma unroll
     for (int j = 0; j < kMaxOut; ++j) {
-      cf[j] = j < n_out ? coef_at(coef_row(P, set, j), k) : CoefK{};
+      // vector loads of the uniform rows (scalar loads of rows the host rewrites between launches
+      // read stale scalar-cache lines, dse_interval.hip at crow)
+      const int nt = j < n_out ? coef_nterm(k, dj[j]) : 0;
+      const double* cc = crow + j * rstride + 2 * (size_t)(k - 1);  // a_{k-2}, a_{k-1}, a_k
+      cf[j].upd = nt > 0;
+      cf[j].c[0] = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0);
+      cf[j].c[1] = nt >= 2 ? make_double2(cc[2], cc[3]) : make_double2(0.0, 0.0);
+      cf[j].c[2] = nt >= 1 ? make_double2(cc[4], cc[5]) : make_double2(0.0, 0.0);
       um |= cf[j].upd ? 1 << j : 0;
       accp[j] = P.racc + ((size_t)(2 * j + comp) << L);
     }
@@ -351,7 +358,7 @@ __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int c
     auto phase5 = [&](auto no_c) {
       constexpr int NO = decltype(no_c)::value;
       constexpr bool ACC = NO > 0 && !(ab & 8);
-      constexpr int NB = R / AB, D = 3;
+      constexpr int NB = R / AB, D = 1;
       const bool first = k == 1;
       double2 av[D][kMaxOut][AB];
       auto issue = [&](int b, int slot) {

@@ -83,3 +83,17 @@ def test_span_kernel_does_not_spill(tmp_path):
     kernels = [k for k in _resources(res.stderr) if "k_span" in k[0]]
     assert len(kernels) >= 4, kernels
     assert all(sp == 0 and sc == 0 for _, sp, sc in kernels), kernels
+
+
+def test_real_kernel_does_not_spill(tmp_path):
+    """k_real (dse_real.hip, option real): the production instantiation k_real<0> holds out and
+    w_{k-2} (32 real rows each) in registers at two waves per SIMD without scratch spills (the
+    diagnostic ablation instantiations may spill)."""
+    res = subprocess.run(
+        [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-c",
+         os.path.join(CSRC, "dse_real.hip"), "-o", str(tmp_path / "real.o"), "-Rpass-analysis=kernel-resource-usage"],
+        capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr[-2000:]
+    kernels = [k for k in _resources(res.stderr) if "k_realILi0E" in k[0]]
+    assert len(kernels) == 1, _resources(res.stderr)
+    assert all(sp == 0 and sc == 0 for _, sp, sc in kernels), kernels
