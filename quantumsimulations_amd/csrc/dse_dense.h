@@ -79,13 +79,26 @@ size_t sytrd_workspace(int n);
 int sytrd_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* d, double* e, double* tau,
                 double* work);
 // Z = Q Z for the Q of sytrd_lower's reflectors in A (rocsolver_dormtr's left / lower / no-transpose
-// case), blocks of 256 reflectors; work: sytrd_workspace(n) bytes
+// case), blocks of 256 reflectors; work: sytrd_workspace(n) bytes.  off: reflector q (column q of A,
+// unit element at row q + off) -- 1 for sytrd_lower, the bandwidth for sy2sb_lower's panels
 int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, const double* tau, double* Z,
-                int ldz, double* work);
+                int ldz, double* work, int off = 1);
 // A = V diag(lam) V^T (lower triangle of A read, A overwritten): sytrd_lower, rocsolver_dstedc,
 // ormtr_lower.  e, tau: n doubles each; V: n x n, ldv >= n; info: rocsolver_dstedc's
 int eig_sym_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
                   double* e, double* tau, double* work, int* info);
+
+// ---- the two-stage eigensolver (dse_eig2.hip): dense -> band 32 (sy2sb_lower), band ->
+// tridiagonal by bulge chasing (sb2st_lower), rocsolver_dstedc, Z <- Q2 Z (q2_apply), Z <- Q1 Z
+// (ormtr_lower, offset 32).  work: eig2_workspace(n) bytes (the chase's reflectors: ~n^2 / 2
+// doubles); n_cu: compute units (the chase's workgroups are co-resident)
+size_t eig2_workspace(int n);
+int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work);
+int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu);
+int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work);
+int eig2_q1(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, double* Z, int ldz, void* work);
+int eig_sym_2stage(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
+                   double* e, void* work, int* info, int n_cu);
 
 }  // namespace dse
 

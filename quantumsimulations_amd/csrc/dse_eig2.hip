@@ -1,0 +1,795 @@
+// dse_eig2.hip -- two-stage symmetric eigendecomposition for the dense engine's large registers
+// (gfx950; option eig_impl = 3).
+//
+// The one-stage tridiagonalisation (dse_sytrd.hip) reads the whole trailing matrix once per column
+// (8 n^3 / 6 bytes: 5.9 TB at n = 2^14, 1.76 s at ~5 TB/s).  Two stages move that work into GEMMs
+// and a cheap chase (prototype and order proofs: tools/proto_two_stage.py):
+//   1. dense -> band b = 32 (sy2sb_lower): panels of b columns; the panel below the band is
+//      QR-factorised (k_panel_qr: one row per thread, one grid barrier per column) and the trailing
+//      matrix updated two-sided by rocBLAS (dsymm, dtrmm, dgemm, dsyr2k): A22 -= V W^T + W V^T,
+//      W = Y - V (T^T V^T Y) / 2, Y = A22 V T.  Reads per panel ~1.5 trailing triangles: 4 n^3 / b
+//      bytes in all (0.55 TB at 2^14).
+//   2. band -> tridiagonal (k_sb2st): bulge chasing, one reflector of length <= b per task (s, t)
+//      (sweep s annihilates column s; task t >= 1 the first column of the bulge block left by task
+//      t - 1), each task a 3b-wide strip of the band held in one wave's LDS.  Sweeps are dealt to
+//      waves; task (s, t) waits until task t + 3 of sweep s - 1 is done (their strips are then
+//      disjoint), so ~n / 4b sweeps run at once.  Band storage: column c, A(c + d, c) at
+//      S[c * kLD + d], d <= 2b (the bulge lives below the band).
+//   3. rocsolver_dstedc on the tridiagonal.
+//   4. Z <- Q2 Z (k_sb_q2): the chase's reflectors in blocks of kQ2NB sweeps (s-blocks last to
+//      first, t ascending, s descending inside a block); a wave owns 64 columns and holds the
+//      block's 64-row window of each in registers, sliding down by b rows per t.
+//   5. Z <- Q1 Z: the panels' reflectors (unit element b rows below their column) by ormtr_lower's
+//      blocks of 256 (dse_sytrd.hip).
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "dse_dense.h"
+
+namespace dse {
+namespace {
+
+constexpr int kB = 32;              // bandwidth of stage 1 = reflector length of stage 2
+constexpr int kLD = 2 * kB + 2;     // band storage per column: d = 0 .. 2b, one pad
+constexpr int kPanelRows = 256;     // panel QR: rows (threads) per workgroup
+constexpr int kQ2NB = 32;           // Q2 application: sweeps per group
+constexpr int kQ2Win = kQ2NB + kB;  // window rows per column
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// LDS writes of other lanes of this wave visible to the reads that follow (no workgroup barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// all co-resident workgroups of the launch reach target (counter monotone within the launch)
+__device__ __forceinline__ void grid_sync(int* cnt, int target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+}
+
+// ---- stage 1 ------------------------------------------------------------------------------------
+
+// Householder QR of the m x kB panel P (column-major, ld lda) in place, LAPACK dgeqr2's layout
+// (R on and above the diagonal, v below it with v_0 = 1 implied, tau[j]).  Thread = row; the
+// workgroups are co-resident (gridDim.x <= CUs), one grid barrier per column.  part: 2 x gridDim.x
+// x (kB + 1) doubles, piv: 2 x kB doubles, cnt zeroed before the launch.
+__global__ void __launch_bounds__(kPanelRows)
+k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
+           double* __restrict__ piv, int* __restrict__ cnt) {
+  __shared__ double red[kPanelRows / 64][kB];
+  __shared__ double tot[kB];
+  __shared__ double prow[kB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = gridDim.x;
+  const int r = blockIdx.x * kPanelRows + tid;
+  const bool own = r < m;
+  double x[kB];
+#pragma unroll
+  for (int k = 0; k < kB; ++k) x[k] = own ? P[(size_t)k * lda + r] : 0.0;
+  const int kmax = min(m, kB);
+  for (int j = 0; j < kmax; ++j) {
+    const int par = j & 1;
+    double* pj = part + ((size_t)par * G + blockIdx.x) * (kB + 1);
+    // slot j: sum of squares of x_j below row j; slot k > j: sum of x_j x_k below row j
+    const bool below = own && r > j;
+    double xj = 0.0;
+#pragma unroll
+    for (int k = 0; k < kB; ++k) xj = k == j ? x[k] : xj;
+    if (!below) xj = 0.0;
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      if (k < j) continue;
+      const double s = wave_sum(xj * x[k]);
+      if (lane == 0) red[wave][k] = s;
+    }
+    if (own && r == j) {
+#pragma unroll
+      for (int k = 0; k < kB; ++k) piv[par * kB + k] = x[k];
+    }
+    __syncthreads();
+    if (tid < kB && tid >= j) pj[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    grid_sync(cnt, (j + 1) * G);
+    if (tid < kB && tid >= j) {
+      double s = 0.0;
+      for (int g = 0; g < G; ++g) s += part[((size_t)par * G + g) * (kB + 1) + tid];
+      tot[tid] = s;
+      prow[tid] = piv[par * kB + tid];
+    }
+    __syncthreads();
+    const double alpha = prow[j], s2 = tot[j];
+    double beta = alpha, t = 0.0, sc = 0.0;
+    if (s2 != 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + s2), alpha);
+      t = (beta - alpha) / beta;
+      sc = 1.0 / (alpha - beta);
+    }
+    if (blockIdx.x == 0 && tid == 0) tau[j] = t;
+    if (t != 0.0) {
+      if (below) {
+        const double v = xj * sc;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          if (k < j) continue;
+          if (k == j) {
+            x[k] = v;
+          } else {
+            const double w = t * (prow[k] + sc * tot[k]);
+            x[k] = fma(-v, w, x[k]);
+          }
+        }
+      } else if (own && r == j) {
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          if (k < j) continue;
+          if (k == j) {
+            x[k] = beta;
+          } else {
+            const double w = t * (prow[k] + sc * tot[k]);
+            x[k] -= w;
+          }
+        }
+      }
+    }
+  }
+  if (own) {
+#pragma unroll
+    for (int k = 0; k < kB; ++k) P[(size_t)k * lda + r] = x[k];
+  }
+}
+
+// Vw (m x k, ld m): the panel's reflectors with their unit diagonal and zeros above
+__global__ void __launch_bounds__(256)
+k_sb_vcopy(const double* __restrict__ P, int lda, int m, int k, double* __restrict__ Vw) {
+  const int r = (int)(blockIdx.x * 256 + threadIdx.x), q = (int)blockIdx.y;  // q < kB: zero past k
+  if (r >= m) return;
+  Vw[(size_t)q * m + r] = q >= k ? 0.0 : r > q ? P[(size_t)q * lda + r] : (r == q ? 1.0 : 0.0);
+}
+
+// ---- stage 1's trailing update on the matrix cores (v_mfma_f64_16x16x4_f64: lane l holds A(l & 15,
+// l >> 4) and B(l >> 4, l & 15) of a 16 x 4 / 4 x 16 step; D(row (l >> 4) + 4 r, col l & 15), r < 4,
+// cdna_hip_programming.md) ----
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kT = 64;       // tile of the trailing matrix
+constexpr int kTP = kT + 4;  // LDS row pitch (doubles): 8 r + 2 k distinct banks over a 16-lane group
+
+__device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Y (m x kB, ld m) = A22 V for the symmetric A22 (lower triangle stored, ld lda), V m x kB (ld m).
+// Workgroup = 64-row block I, 4 waves x 16 rows; tiles J <= I as stored, J > I transposed (A_JI^T).
+__global__ void __launch_bounds__(256)
+k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict__ V, double* __restrict__ Y) {
+  __shared__ double T[kT][kTP];
+  __shared__ double Vt[kT][kB + 4];
+  const int I = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nbk = (m + kT - 1) / kT;
+  const int r0 = I * kT;
+  f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  for (int J = 0; J < nbk; ++J) {
+    const int c0 = J * kT;
+    __syncthreads();
+    // T(r, c) = A(r0 + r, c0 + c) from the lower triangle: stored at column min, row max
+    for (int e = tid; e < kT * kT; e += 256) {
+      const int a = e & 63, b = e >> 6;  // a: fast index
+      int r, c;
+      if (J <= I) r = a, c = b;  // column-major reads of A(r0 + r, c0 + c), rows contiguous
+      else r = b, c = a;         // A(c0 + c, r0 + r) is stored: contiguous in c
+      const int gr = r0 + r, gc = c0 + c;
+      double v = 0.0;
+      if (gr < m && gc < m) v = gr >= gc ? A[(size_t)gc * lda + gr] : A[(size_t)gr * lda + gc];
+      T[r][c] = v;
+    }
+    for (int e = tid; e < kT * kB; e += 256) {
+      const int c = e & 63, k = e >> 6;
+      Vt[c][k] = c0 + c < m ? V[(size_t)k * m + c0 + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kT / 4; ++kk) {
+      const double a = T[16 * w + (lane & 15)][4 * kk + (lane >> 4)];
+      acc0 = mfma64(a, Vt[4 * kk + (lane >> 4)][lane & 15], acc0);
+      acc1 = mfma64(a, Vt[4 * kk + (lane >> 4)][16 + (lane & 15)], acc1);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = r0 + 16 * w + (lane >> 4) + 4 * r;
+    if (row < m) {
+      Y[(size_t)(lane & 15) * m + row] = acc0[r];
+      Y[(size_t)(16 + (lane & 15)) * m + row] = acc1[r];
+    }
+  }
+}
+
+// A22 (lower, ld lda) -= V W^T + W V^T on the 64 x 64 tiles on and below the diagonal: D' = Q P^T
+// with P = [V_I | W_I], Q = [W_J | V_J] (64 x 2 kB each); D'(c, r) -= into A(I 64 + r, J 64 + c),
+// lanes along r (contiguous rows of column-major A)
+__global__ void __launch_bounds__(256)
+k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ V, const double* __restrict__ W) {
+  const int I = blockIdx.x, J = blockIdx.y;
+  if (J > I) return;
+  __shared__ double P[kT][kTP];
+  __shared__ double Q[kT][kTP];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = I * kT, c0 = J * kT;
+  for (int e = tid; e < kT * kB; e += 256) {
+    const int r = e & 63, k = e >> 6;
+    const bool ri = r0 + r < m, cj = c0 + r < m;
+    P[r][k] = ri ? V[(size_t)k * m + r0 + r] : 0.0;
+    P[r][kB + k] = ri ? W[(size_t)k * m + r0 + r] : 0.0;
+    Q[r][k] = cj ? W[(size_t)k * m + c0 + r] : 0.0;
+    Q[r][kB + k] = cj ? V[(size_t)k * m + c0 + r] : 0.0;
+  }
+  __syncthreads();
+  f64x4 acc[4];
+#pragma unroll
+  for (int sc = 0; sc < 4; ++sc) acc[sc] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 2 * kB / 4; ++kk) {
+    const double a = Q[16 * w + (lane & 15)][4 * kk + (lane >> 4)];
+#pragma unroll
+    for (int sc = 0; sc < 4; ++sc) acc[sc] = mfma64(a, P[16 * sc + (lane & 15)][4 * kk + (lane >> 4)], acc[sc]);
+  }
+#pragma unroll
+  for (int sc = 0; sc < 4; ++sc)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gc = c0 + 16 * w + (lane >> 4) + 4 * r, gr = r0 + 16 * sc + (lane & 15);
+      if (gr < m && gc < m && gr >= gc) A[(size_t)gc * lda + gr] -= acc[sc][r];
+    }
+}
+
+// Y <- Y T (T kB x kB upper, ld kB) row-wise in place (small: m kB^2 / 2 FMAs; rows in LDS)
+__global__ void __launch_bounds__(256)
+k_sb_yt(double* __restrict__ Y, int m, int k, const double* __restrict__ T) {
+  __shared__ double Ts[kB][kB + 1];
+  __shared__ double Ys[kB][256 + 1];
+  const int tid = threadIdx.x, r = blockIdx.x * 256 + tid;
+  for (int e = tid; e < kB * kB; e += 256) {
+    const int i = e % kB, j = e / kB;
+    Ts[i][j] = (i < k && j < k && i <= j) ? T[(size_t)j * kB + i] : 0.0;
+  }
+  for (int q = 0; q < kB; ++q) Ys[q][tid] = (r < m && q < k) ? Y[(size_t)q * m + r] : 0.0;
+  __syncthreads();
+  if (r >= m) return;
+  for (int q = 0; q < k; ++q) {
+    double a = 0.0;
+    for (int p = 0; p <= q; ++p) a = fma(Ys[p][tid], Ts[p][q], a);
+    Y[(size_t)q * m + r] = a;
+  }
+}
+
+// part[g] (kB x kB, column-major) = V_g^T Y_g over the 256-row chunk g, on the matrix cores
+// (4 waves: wave w takes the chunk's rows 64 w .. 64 w + 63, the four 16 x 16 output tiles; the
+// waves' sums are added in fixed order)
+__global__ void __launch_bounds__(256)
+k_sb_vty(const double* __restrict__ V, const double* __restrict__ Y, int m, double* __restrict__ part) {
+  __shared__ double Vs[256][kB + 4];
+  __shared__ double Ys[256][kB + 4];
+  double(*red)[kB * kB] = reinterpret_cast<double(*)[kB * kB]>(&Vs[0][0]);  // after the products
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rb = blockIdx.x * 256;
+  for (int e = tid; e < 256 * kB; e += 256) {
+    const int r = e & 255, q = e >> 8;
+    const bool ok = rb + r < m;
+    Vs[r][q] = ok ? V[(size_t)q * m + rb + r] : 0.0;
+    Ys[r][q] = ok ? Y[(size_t)q * m + rb + r] : 0.0;
+  }
+  __syncthreads();
+  // D(p, q) = sum_r V(r, p) Y(r, q): A(i = p, kk = r) = V(r, p), B(kk = r, j = q) = Y(r, q)
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int r = 64 * w + 4 * kk + (lane >> 4);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const double va = Vs[r][16 * a + (lane & 15)];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = mfma64(va, Ys[r][16 * b + (lane & 15)], acc[a][b]);
+    }
+  }
+  __syncthreads();  // every wave's reads of Vs done before red overwrites it
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int p = 16 * a + (lane >> 4) + 4 * rr, q = 16 * b + (lane & 15);
+        red[w][q * kB + p] = acc[a][b][rr];
+      }
+  __syncthreads();
+  for (int e = tid; e < kB * kB; e += 256)
+    part[(size_t)blockIdx.x * kB * kB + e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+}
+
+// Gm = T^T M, M = sum of the partials (fixed order); one workgroup
+__global__ void __launch_bounds__(kB * kB)
+k_sb_gm(const double* __restrict__ part, int ng, int k, const double* __restrict__ T, double* __restrict__ Gm) {
+  __shared__ double M[kB][kB];
+  const int e = threadIdx.x, p = e % kB, q = e / kB;
+  double a = 0.0;
+  for (int g = 0; g < ng; ++g) a += part[(size_t)g * kB * kB + e];
+  M[p][q] = a;
+  __syncthreads();
+  double gsum = 0.0;
+  for (int i = 0; i <= p; ++i) gsum = fma(T[(size_t)p * kB + i], M[i][q], gsum);  // T^T(p, i) = T(i, p)
+  Gm[(size_t)q * kB + p] = (p < k && q < k) ? gsum : 0.0;
+}
+
+// W = Y2 - V Gm / 2 row-wise in place (into Y)
+__global__ void __launch_bounds__(256)
+k_sb_w(double* __restrict__ Y, const double* __restrict__ V, int m, int k, const double* __restrict__ Gm) {
+  __shared__ double Gs[kB][kB];
+  const int tid = threadIdx.x, r = blockIdx.x * 256 + tid;
+  for (int e = tid; e < kB * kB; e += 256) Gs[e % kB][e / kB] = Gm[e];
+  __syncthreads();
+  if (r >= m) return;
+  double v[kB];
+#pragma unroll
+  for (int p = 0; p < kB; ++p) v[p] = p < k ? V[(size_t)p * m + r] : 0.0;
+#pragma unroll
+  for (int q = 0; q < kB; ++q) {
+    if (q >= k) continue;
+    double a = 0.0;
+#pragma unroll
+    for (int p = 0; p < kB; ++p) a = fma(v[p], Gs[p][q], a);
+    Y[(size_t)q * m + r] -= 0.5 * a;
+  }
+}
+
+// band storage S[c * kLD + d] = A(c + d, c) for d <= kB (0 beyond, room for the bulge)
+__global__ void __launch_bounds__(256)
+k_sb_band(const double* __restrict__ A, int lda, int n, double* __restrict__ S) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (size_t)n * kLD) return;
+  const int c = (int)(e / kLD), d = (int)(e % kLD);
+  S[e] = (d <= kB && c + d < n) ? A[(size_t)c * lda + c + d] : 0.0;
+}
+
+// ---- stage 2 ------------------------------------------------------------------------------------
+
+__host__ __device__ __forceinline__ int chase_tasks(int n, int s) { return 1 + (n - 2 - s) / kB; }
+
+// Reflector (s, t) of the chase in group-major order for the Q2 application: group (block, t) of
+// sweeps s in [block kQ2NB, block kQ2NB + kQ2NB) is kQ2NB consecutive records (v[kB], tau, pad:
+// kRec doubles, v 16-B aligned) starting at goff[block] + t kQ2NB kRec; absent reflectors stay
+// zero (tau = 0).
+constexpr int kRec = kB + 2;
+__device__ __forceinline__ double* refl_at(double* refl, const long long* goff, int s, int t) {
+  return refl + goff[s / kQ2NB] + ((size_t)t * kQ2NB + (s % kQ2NB)) * kRec;
+}
+
+// One task (s, t) by one wave, the three 32 x 32 blocks in registers: lane = column j (L, D) or row
+// i (R) of a 16-row / 16-column half h = lane >> 5.  v, w and the annihilated column in LDS.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t band_rsrc(double* S, int n) {
+  const uint64_t a = (uint64_t)S;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)((size_t)n * kLD * 8),
+                                           0x00020000);
+}
+// band element e (32-bit index) with sc1 loads and stores: the chase hands the band between CUs in
+// the guide's valid form (MI355X_MICROARCH.md "Valid forms", row 1, per wave: every load and
+// store of the band sc1, each storing wave's s_waitcnt vmcnt(0) before its sc1 flag store, the
+// consumer wave polls the flag with sc1 loads and then loads)
+constexpr int kBandSc1 = 16;  // aux: sc1 (dse_device.h kSc1)
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int e) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, e * 8, 0, kBandSc1));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int e, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, e * 8, 0, kBandSc1);
+}
+
+struct ChaseVec {
+  double x[kB];
+  double v[kB];
+  double w[kB];
+};
+
+__device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec& B, double* __restrict__ rf) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, h = lane >> 5, i0 = 16 * h;
+  const int col = t == 0 ? s : s + (t - 1) * kB + 1;
+  const int r0 = t == 0 ? s + 1 : s + t * kB + 1;
+  const int m = min(kB, n - r0);
+  const int nL = t == 0 ? 1 : kB;
+  const int mr = max(0, min(kB, n - r0 - m));
+  const __amdgpu_buffer_rsrc_t rs = band_rsrc(S, n);
+  double Lc[16], Dc[16], Rr[16];
+  // L(i, j) = A(r0 + i, col + j); D(i, j) = A(r0 + i, r0 + j); R(i, jj) = A(r0 + m + i, r0 + jj)
+  const int eL = (col + j) * kLD + (r0 - col - j) + i0;  // + q
+  const int eD = (r0 + j) * kLD + (i0 - j);              // + q, rows i >= j
+  const int eDu = (r0 + i0) * kLD + (j - i0);            // + q (kLD - 1), rows i < j
+  const int eR = (r0 + i0) * kLD + (m + j - i0);         // + q (kLD - 1)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = i0 + q;
+    Lc[q] = (i < m && j < nL) ? bload(rs, eL + q) : 0.0;
+    double dv = 0.0;
+    if (i < m && j < m) dv = i >= j ? bload(rs, eD + q) : bload(rs, eDu + q * (kLD - 1));
+    Dc[q] = dv;
+    const int jj = i0 + q;
+    Rr[q] = (j < mr && jj < m) ? bload(rs, eR + q * (kLD - 1)) : 0.0;
+  }
+  // the reflector of L(:, 0)
+  if (j == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) B.x[i0 + q] = Lc[q];
+  }
+  wave_sync();
+  const double xi = lane < kB ? B.x[lane] : 0.0;
+  const double alpha = B.x[0];
+  const double s2 = wave_sum((lane >= 1 && lane < m) ? xi * xi : 0.0);
+  double beta = alpha, tau = 0.0, sc = 0.0;
+  if (s2 != 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + s2), alpha);
+    tau = (beta - alpha) / beta;
+    sc = 1.0 / (alpha - beta);
+  }
+  if (lane < kB) B.v[lane] = lane == 0 ? 1.0 : (lane < m ? xi * sc : 0.0);
+  wave_sync();
+  if (tau != 0.0) {
+    double vh[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) vh[q] = B.v[i0 + q];
+    const double vj = B.v[j];
+    // L <- H L (columns 1 ..; column 0 becomes beta e1)
+    {
+      double p = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) p = fma(vh[q], Lc[q], p);
+      const double wl = tau * (p + __shfl_xor(p, 32, 64));
+      if (j == 0) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Lc[q] = (h == 0 && q == 0) ? beta : 0.0;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Lc[q] = fma(-wl, vh[q], Lc[q]);
+      }
+    }
+    // D <- H D H: y_j = D(:, j) . v (symmetric), w = tau y - tau^2 (v . y) v / 2,
+    // D -= v w^T + w v^T
+    {
+      double p = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) p = fma(vh[q], Dc[q], p);
+      const double y = p + __shfl_xor(p, 32, 64);
+      const double K = wave_sum(lane < kB ? vj * y : 0.0);
+      const double wj = tau * y - 0.5 * tau * tau * K * vj;
+      if (lane < kB) B.w[lane] = wj;
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Dc[q] -= vh[q] * wj + B.w[i0 + q] * vj;
+    }
+    // R <- R H (lane = row j, columns of half h): z = R(j, :) . v, R(j, :) -= tau z v^T
+    {
+      double p = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) p = fma(vh[q], Rr[q], p);
+      const double z = tau * (p + __shfl_xor(p, 32, 64));
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Rr[q] = fma(-z, vh[q], Rr[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = i0 + q;
+      if (i < m && j < nL) bstore(rs, eL + q, Lc[q]);
+      if (i < m && j < m && i >= j) bstore(rs, eD + q, Dc[q]);
+      const int jj = i0 + q;
+      if (j < mr && jj < m) bstore(rs, eR + q * (kLD - 1), Rr[q]);
+    }
+  }
+  if (lane == 0) rf[kB] = tau;
+  if (lane < kB) rf[lane] = B.v[lane];
+  wave_sync();
+}
+
+// Workers = waves (kChaseWG per workgroup, the workgroups spread over the chip); worker w takes
+// sweeps w, w + W, ...; task (s, t) waits until sweep s - 1 has finished task t + 2 (or all its
+// tasks): the strips of (s, t) and (s - 1, t + 3) share no entry (tools/proto_two_stage.py).
+// prog[s] = tasks of sweep s done (zeroed before); relaxed agent-scope (sc1) flag stores and polls.
+constexpr int kChaseWG = 4;  // waves per chase workgroup
+__global__ void __launch_bounds__(64 * kChaseWG)
+k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long long* __restrict__ goff,
+        int* __restrict__ prog) {
+  __shared__ ChaseVec lds[kChaseWG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int W = gridDim.x * kChaseWG, w = blockIdx.x * kChaseWG + wv;
+  ChaseVec& B = lds[wv];
+  for (int s = w; s < n - 1; s += W) {
+    const int nt = chase_tasks(n, s);
+    const int ntp = s > 0 ? chase_tasks(n, s - 1) : 0;
+    for (int t = 0; t < nt; ++t) {
+      if (s > 0) {
+        const int need = min(ntp, t + 3);
+        while (__hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      chase_task(S, n, s, t, B, refl_at(refl, goff, s, t));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(prog + s, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// d, e of the tridiagonal from the band
+__global__ void k_sb_tridiag(const double* __restrict__ S, int n, double* __restrict__ d, double* __restrict__ e) {
+  const int c = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (c >= n) return;
+  d[c] = S[(size_t)c * kLD];
+  e[c] = c + 1 < n ? S[(size_t)c * kLD + 1] : 0.0;
+}
+
+// ---- Z <- Q2 Z ----------------------------------------------------------------------------------
+
+// 64 columns (lane = column) per workgroup of kQ2Waves waves.  Blocks of kQ2NB sweeps are applied
+// from the last to the first; block i of that order (i = 0, 1, ...) goes to wave i % kQ2Waves, which
+// trails the wave of block i - 1 by one group: group t of block i needs block i - 1's group t done
+// (its window has then moved below every row group t touches; tools/proto_two_stage.py's order).
+// In a block, t ascending; the group (block, t)'s reflectors (s descending) act on window rows
+// lo .. lo + 62, lo = s0 + t b + 1, reflector s at window offset s - s0 (compile time).  The next
+// group's records (contiguous, refl_at) are loaded into registers while this group is applied.
+// Waves of one workgroup hand rows over through L2: plain stores, s_waitcnt vmcnt(0), then the LDS
+// progress word; the reader's window loads are sc1 (past the CU's L1).
+constexpr int kQ2Rec = kQ2NB * kRec;             // doubles per group
+constexpr int kQ2PerLane = (kQ2Rec + 63) / 64;    // staging loads per lane
+constexpr int kQ2Waves = 4;
+__global__ void __launch_bounds__(64 * kQ2Waves)
+k_sb_q2(double* __restrict__ Z, int ldz, int n, const double* __restrict__ refl, const long long* __restrict__ goff) {
+  __shared__ __attribute__((aligned(16))) double rvs[kQ2Waves][kQ2PerLane * 64];
+  __shared__ int state[kQ2Waves];  // (block order index) * 65536 + groups done (65535: block done)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double* rv = rvs[wv];
+  const int colg = blockIdx.x * 64 + lane;
+  const bool live = colg < n;
+  double* zc = Z + (size_t)(live ? colg : 0) * ldz;
+  const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)Z >> 32)) << 32) |
+              __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)Z)),
+      0, 0x7fffffff, 0x00020000);
+  const uint32_t cbase = (uint32_t)((size_t)(live ? colg : 0) * ldz);  // element offset of the column
+  auto zld = [&](int row) -> double {  // sc1: another wave of this CU may have rewritten the line
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, (int)((cbase + (uint32_t)row) * 8u),
+                                                                            0, kBandSc1));
+  };
+  if (lane == 0) state[wv] = -1;
+  __syncthreads();
+  const int ns = n - 1;
+  const int nblk = (ns + kQ2NB - 1) / kQ2NB;
+  const int pw = (wv + kQ2Waves - 1) % kQ2Waves;  // the wave of the previous block
+  for (int i = wv; i < nblk; i += kQ2Waves) {
+    const int blk = nblk - 1 - i;
+    const int s0 = blk * kQ2NB;
+    const int T0 = chase_tasks(n, s0);
+    auto wait_prev = [&](int t) {  // block i - 1 has finished group t (or the whole block)
+      if (i == 0) return;
+      const int need = (i - 1) * 65536 + min(t + 1, 65535);
+      while (__hip_atomic_load(&state[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+        __builtin_amdgcn_s_sleep(1);
+    };
+    const double* gb = refl + goff[blk];
+    double pre[kQ2PerLane];
+#pragma unroll
+    for (int q = 0; q < kQ2PerLane; ++q) {
+      const int e = q * 64 + lane;
+      pre[q] = e < kQ2Rec ? gb[e] : 0.0;
+    }
+    double win[kQ2Win];
+    int lo = s0 + 1;
+    wait_prev(0);
+#pragma unroll
+    for (int r = 0; r < kQ2Win; ++r) win[r] = (live && lo + r < n) ? zld(lo + r) : 0.0;
+    for (int t = 0; t < T0; ++t) {
+#pragma unroll
+      for (int q = 0; q < kQ2PerLane; ++q) rv[q * 64 + lane] = pre[q];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (t + 1 < T0) {
+        const double* g = gb + (size_t)(t + 1) * kQ2Rec;
+#pragma unroll
+        for (int q = 0; q < kQ2PerLane; ++q) {
+          const int e = q * 64 + lane;
+          pre[q] = e < kQ2Rec ? g[e] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = kQ2NB - 1; u >= 0; --u) {
+        const double* r = rv + u * kRec;
+        const double tau = r[kB];
+        if (tau == 0.0) continue;  // uniform
+        double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+#pragma unroll
+        for (int k = 0; k < kB; k += 4) {
+          d0 = fma(r[k], win[u + k], d0);
+          d1 = fma(r[k + 1], win[u + k + 1], d1);
+          d2 = fma(r[k + 2], win[u + k + 2], d2);
+          d3 = fma(r[k + 3], win[u + k + 3], d3);
+        }
+        const double g = tau * ((d0 + d1) + (d2 + d3));
+#pragma unroll
+        for (int k = 0; k < kB; ++k) win[u + k] = fma(-g, r[k], win[u + k]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // slide: rows lo .. lo + b - 1 are final for this block
+#pragma unroll
+      for (int r = 0; r < kB; ++r)
+        if (live && lo + r < n) zc[lo + r] = win[r];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int r = 0; r < kQ2Win - kB; ++r) win[r] = win[r + kB];
+      lo += kB;
+      if (t + 1 < T0) wait_prev(t + 1);
+#pragma unroll
+      for (int r = kQ2Win - kB; r < kQ2Win; ++r) win[r] = (live && lo + r < n) ? zld(lo + r) : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < kQ2Win; ++r)
+      if (live && lo + r < n) zc[lo + r] = win[r];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + 65535, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+struct Eig2Ws {
+  double* tau1;     // n: stage-1 reflectors (zero where none)
+  double* T;        // panels x b x b
+  double* Vw;       // n x b
+  double* Y;        // n x b
+  double* M;        // b x b
+  double* Gm;       // b x b
+  double* part;     // 2 x 128 x (b + 1)
+  double* part2;    // (n / 256 + 2) x b x b: V^T Y partials
+  double* piv;      // 2 x b
+  double* S;        // n x kLD band
+  double* refl;     // chase reflectors x (b + 1)
+  double* orm;      // ormtr_lower workspace
+  long long* goff;  // n / kQ2NB + 1: group-major reflector offsets per block of sweeps
+  int* prog;        // n
+  int* cnt;         // 1
+};
+
+// doubles of the group-major reflector records: per block of kQ2NB sweeps, chase_tasks(first
+// sweep) groups of kQ2NB records
+size_t chase_refl_doubles(int n, std::vector<long long>* goff = nullptr) {
+  const int ns = n - 1, nblk = (ns + kQ2NB - 1) / kQ2NB;
+  size_t k = 0;
+  if (goff) goff->assign(nblk + 1, 0);
+  for (int b = 0; b < nblk; ++b) {
+    if (goff) (*goff)[b] = (long long)k;
+    k += (size_t)chase_tasks(n, b * kQ2NB) * kQ2NB * kRec;
+  }
+  if (goff) (*goff)[nblk] = (long long)k;
+  return k;
+}
+
+// the workspace's arrays from base (nullptr: offsets only, for the size)
+Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
+  const int panels = n / kB + 1;
+  size_t off = 0;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(work);
+  auto take = [&](size_t b) {
+    const size_t o = off;
+    off += (b + 255) / 256 * 256;
+    return reinterpret_cast<void*>(base + o);
+  };
+  Eig2Ws w;
+  w.tau1 = (double*)take((size_t)n * 8);
+  w.T = (double*)take((size_t)panels * kB * kB * 8);
+  w.Vw = (double*)take((size_t)n * kB * 8);
+  w.Y = (double*)take((size_t)n * kB * 8);
+  w.M = (double*)take((size_t)kB * kB * 8);
+  w.Gm = (double*)take((size_t)kB * kB * 8);
+  w.part = (double*)take((size_t)2 * 128 * (kB + 1) * 8);
+  w.piv = (double*)take((size_t)2 * kB * 8);
+  w.part2 = (double*)take(((size_t)n / 256 + 2) * kB * kB * 8);
+  w.S = (double*)take((size_t)n * kLD * 8);
+  w.refl = (double*)take(chase_refl_doubles(n) * 8);
+  w.orm = (double*)take(sytrd_workspace(n));
+  w.goff = (long long*)take(((size_t)n / kQ2NB + 2) * 8);
+  w.prog = (int*)take((size_t)n * 4);
+  w.cnt = (int*)take(256);
+  if (bytes) *bytes = off;
+  return w;
+}
+
+}  // namespace
+
+size_t eig2_workspace(int n) {
+  size_t b = 0;
+  carve2(nullptr, n, &b);
+  return b;
+}
+
+int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work) {
+  Eig2Ws ws = carve2(work, n);
+  if (hipMemsetAsync(ws.tau1, 0, (size_t)n * 8, st) != hipSuccess) return -1;
+  int p = 0;
+  for (int i = 0; i < n - kB - 1; i += kB, ++p) {
+    const int m = n - i - kB;
+    double* P = A + (size_t)i * lda + i + kB;
+    const int G = (m + kPanelRows - 1) / kPanelRows;
+    if (G > 128) return -2;
+    if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, st, P, lda, m, ws.tau1 + i, ws.part, ws.piv, ws.cnt);
+    if (hipGetLastError() != hipSuccess) return -1;
+    const int k = std::min(m, kB);
+    double* T = ws.T + (size_t)p * kB * kB;
+    if (rocsolver_dlarft(h, rocblas_forward_direction, rocblas_column_wise, m, k, P, lda, ws.tau1 + i, T, kB) !=
+        rocblas_status_success)
+      return -3;
+    hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256, kB), dim3(256), 0, st, P, lda, m, k, ws.Vw);
+    double* A22 = A + (size_t)(i + kB) * lda + i + kB;
+    const int nbk = (m + kT - 1) / kT, ng = (m + 255) / 256;
+    // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
+    hipLaunchKernelGGL(k_sb_symm, dim3(nbk), dim3(256), 0, st, A22, lda, m, ws.Vw, ws.Y);
+    hipLaunchKernelGGL(k_sb_yt, dim3(ng), dim3(256), 0, st, ws.Y, m, k, T);
+    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Y, m, ws.part2);
+    hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
+    hipLaunchKernelGGL(k_sb_w, dim3(ng), dim3(256), 0, st, ws.Y, ws.Vw, m, k, ws.Gm);
+    hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, ws.Vw, ws.Y);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu) {
+  Eig2Ws ws = carve2(work, n);
+  std::vector<long long> goff;
+  const size_t nrefl = chase_refl_doubles(n, &goff);
+  if (hipMemcpyAsync(ws.goff, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
+  if (hipMemsetAsync(ws.refl, 0, nrefl * 8, st) != hipSuccess) return -1;
+  if (hipMemsetAsync(ws.prog, 0, (size_t)n * 4, st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_sb_band, dim3((unsigned)(((size_t)n * kLD + 255) / 256)), dim3(256), 0, st, A, lda, n, ws.S);
+  // ~n / (3 b) sweeps run at once: one worker per 2 b columns, at most one workgroup per CU
+  const int nwg = std::max(1, std::min(n_cu, (n + 2 * kB * kChaseWG - 1) / (2 * kB * kChaseWG)));
+  hipLaunchKernelGGL(k_sb2st, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog);
+  hipLaunchKernelGGL(k_sb_tridiag, dim3((n + 255) / 256), dim3(256), 0, st, ws.S, n, d, e);
+  if (hipStreamSynchronize(st) != hipSuccess) return -1;  // goff is host memory until here
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
+  Eig2Ws ws = carve2(work, n);
+  hipLaunchKernelGGL(k_sb_q2, dim3((n + 63) / 64), dim3(64 * kQ2Waves), 0, st, Z, ldz, n, ws.refl, ws.goff);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int eig2_q1(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, double* Z, int ldz, void* work) {
+  Eig2Ws ws = carve2(work, n);
+  return ormtr_lower(h, st, n, A, lda, ws.tau1, Z, ldz, ws.orm, kB);
+}
+
+int eig_sym_2stage(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
+                   double* e, void* work, int* info, int n_cu) {
+  int rc = sy2sb_lower(h, st, n, A, lda, work);
+  if (rc) return rc;
+  if ((rc = sb2st_lower(st, n, A, lda, lam, e, work, n_cu))) return rc;
+  if (rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, ldv, info) != rocblas_status_success) return -8;
+  if ((rc = q2_apply(st, n, V, ldv, work))) return rc;
+  return eig2_q1(h, st, n, A, lda, V, ldv, work);
+}
+
+}  // namespace dse

@@ -399,14 +399,15 @@ k_trd_wfix(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int 
 constexpr int kOrmKB = 256;
 constexpr int kHalfTrdMinDim = 8192;
 
-// Vb (m_b x k, column-major): unit lower trapezoid of the reflectors i .. i+k-1 (rows i+1 .. n-1)
+// Vb (m_b x k, column-major): unit lower trapezoid of the reflectors i .. i+k-1 (reflector q of
+// column i + q starts at row i + q + off: rows i + off .. n-1)
 __global__ void __launch_bounds__(256)
-k_orm_vb(const double* __restrict__ A, int lda, const double* __restrict__ tau, int i, int k, int m_b,
+k_orm_vb(const double* __restrict__ A, int lda, const double* __restrict__ tau, int i, int k, int m_b, int off,
          double* __restrict__ Vb) {
   const int r = (int)(blockIdx.x * 256 + threadIdx.x), q = (int)blockIdx.y;
   if (r >= m_b) return;
   double v = 0.0;
-  if (tau[i + q] != 0.0) v = r > q ? A[(size_t)(i + q) * lda + (i + 1 + r)] : r == q ? 1.0 : 0.0;
+  if (tau[i + q] != 0.0) v = r > q ? A[(size_t)(i + q) * lda + (i + off + r)] : r == q ? 1.0 : 0.0;
   Vb[(size_t)q * m_b + r] = v;
 }
 
@@ -442,8 +443,8 @@ size_t sytrd_workspace(int n) {
 }
 
 int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, const double* tau, double* Z,
-                int ldz, double* work) {
-  const int nref = n - 1;
+                int ldz, double* work, int off) {
+  const int nref = n - off;
   if (nref <= 0) return 0;
   double* Vb = work;
   double* Wt = Vb + (size_t)n * kOrmKB;
@@ -451,21 +452,21 @@ int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int ld
   const double one = 1.0, zero = 0.0, minus_one = -1.0;
   const int nblk = (nref + kOrmKB - 1) / kOrmKB;
   for (int b = nblk - 1; b >= 0; --b) {
-    const int i = b * kOrmKB, k = std::min(kOrmKB, nref - i), m_b = n - i - 1;
-    hipLaunchKernelGGL(k_orm_vb, dim3((m_b + 255) / 256, k), dim3(256), 0, st, A, lda, tau, i, k, m_b, Vb);
+    const int i = b * kOrmKB, k = std::min(kOrmKB, nref - i), m_b = n - i - off;
+    hipLaunchKernelGGL(k_orm_vb, dim3((m_b + 255) / 256, k), dim3(256), 0, st, A, lda, tau, i, k, m_b, off, Vb);
     if (hipGetLastError() != hipSuccess) return -6;
     if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, k, k, m_b, &one, Vb, m_b, Vb, m_b, &zero,
                       S, k) != rocblas_status_success)
       return -7;
     hipLaunchKernelGGL(k_orm_sdiag, dim3((k + 255) / 256), dim3(256), 0, st, S, k, tau, i);
-    if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, k, n, m_b, &one, Vb, m_b, Z + i + 1, ldz,
-                      &zero, Wt, k) != rocblas_status_success)
+    if (rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, k, n, m_b, &one, Vb, m_b, Z + i + off,
+                      ldz, &zero, Wt, k) != rocblas_status_success)
       return -7;
     if (rocblas_dtrsm(h, rocblas_side_left, rocblas_fill_upper, rocblas_operation_none, rocblas_diagonal_non_unit, k,
                       n, &one, S, k, Wt, k) != rocblas_status_success)
       return -8;
     if (rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, m_b, n, k, &minus_one, Vb, m_b, Wt, k, &one,
-                      Z + i + 1, ldz) != rocblas_status_success)
+                      Z + i + off, ldz) != rocblas_status_success)
       return -7;
   }
   return hipGetLastError() == hipSuccess ? 0 : -6;

@@ -13,6 +13,7 @@
 #   traffic_large              the same over tools/bench_large.py (N = 30, Walsh-Hadamard engine)
 #   sq:<set>                   three SQ counter passes over tools/probe_one.py <set>
 #   sytrd:<dim,...>            tools/bin/probe_sytrd <dim> check
+#   eig2:<dim[/random],...>    tools/bin/probe_eig2 (two-stage eigensolver vs dsyevd)
 #   py:<script>,<args...>      python -u <script> <args> > <tag>/<script-name>.out
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -65,6 +66,14 @@ for T in "$@"; do
       [ $rc -eq 0 ] || fail sq p2
       pmc ${q}p3 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE; rc=$?
       [ $rc -eq 0 ] || fail sq p3 ;;
+    eig2)  # eig2:<dim>[/random],...  tools/bin/probe_eig2 (two-stage eigensolver) against dsyevd
+      for a in "${A[@]}"; do
+        timeout -k 10 ${EIG2_TIMEOUT:-120} tools/bin/probe_eig2 ${a%%/*} $([ "$a" != "${a#*/}" ] && echo ${a#*/}) >> $OUT/eig2.jsonl 2>> $OUT/eig2.err; rc=$?
+        tail -1 $OUT/eig2.jsonl; [ $rc -eq 0 ] || { tail -5 $OUT/eig2.err; fail eig2 $a; }
+      done ;;
+    eig2prof)  # rocprofv3 kernel trace of probe_eig2 <dim>
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/eig2prof_$arg -o eig2 --output-format csv -- tools/bin/probe_eig2 $arg > $OUT/eig2prof_$arg.out 2> $OUT/eig2prof_$arg.err; rc=$?
+      tail -2 $OUT/eig2prof_$arg.out; [ $rc -eq 0 ] || fail eig2prof ;;
     sytrd)
       for n in "${A[@]}"; do
         timeout -k 10 200 tools/bin/probe_sytrd $n check >> $OUT/sytrd.jsonl 2>> $OUT/sytrd.err; rc=$?

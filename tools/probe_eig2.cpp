@@ -1,0 +1,161 @@
+// Probe (round 4): the two-stage eigensolver (dse_eig2.hip) against rocSOLVER dsyevd.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iquantumsimulations_amd/csrc tools/probe_eig2.cpp \
+//         quantumsimulations_amd/csrc/dse_eig2.hip quantumsimulations_amd/csrc/dse_sytrd.hip \
+//         -lrocsolver -lrocblas -o tools/bin/probe_eig2
+//   probe_eig2 <dim> [random]
+// Matrix: tools/probe_sytrd.cpp's (spectrum and sparsity of the N = 14 rotated H') or, with
+// "random", a dense symmetric one.  One JSON line per stage timing, then the check: max |lam -
+// lam_dsyevd| / max |lam|, max |A V - V diag(lam)| / max |lam|, max |V^T V - I|.
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "dse_dense.h"
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(2);                                                                  \
+    }                                                                                \
+  } while (0)
+
+__global__ void k_fill(double* A, int dim, int nbits, unsigned seed) {
+  const unsigned x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= (unsigned)dim) return;
+  double* col = A + (size_t)x * dim;
+  double d = 0.0;
+  for (int b = 0; b < nbits; ++b) d += (0.5 - (double)((x >> b) & 1u)) * (1.0 + 0.37 * b);
+  unsigned h = x * 2654435761u ^ seed;
+  h ^= h >> 15;
+  d += 1e-3 * (double)(h & 1023u);
+  col[x] = d;
+  for (int b = 0; b < nbits; ++b)
+    if ((x ^ (1u << b)) < (unsigned)dim) col[x ^ (1u << b)] = 0.25;
+  for (int i = 0; i < nbits; ++i)
+    for (int j = i + 1; j < nbits; ++j)
+      if (!(((x >> i) ^ (x >> j)) & 1u) && (x ^ ((1u << i) | (1u << j))) < (unsigned)dim)
+        col[x ^ ((1u << i) | (1u << j))] = -0.01 * (1 + ((i * 7 + j) % 5));
+}
+
+__global__ void k_rand(double* A, int dim, unsigned seed) {
+  const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= (size_t)dim * dim) return;
+  const unsigned r = (unsigned)(k % dim), c = (unsigned)(k / dim);
+  const unsigned a = std::min(r, c), b = std::max(r, c);
+  unsigned h = (a * 2654435761u) ^ (b * 40503u) ^ seed;
+  h ^= h >> 13;
+  h *= 0x5bd1e995u;
+  h ^= h >> 15;
+  A[k] = (double)(h & 0xffffu) / 65536.0 - 0.5;
+}
+
+__global__ void k_eye(double* R, int dim) {
+  const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= (size_t)dim * dim) return;
+  R[k] = (k % dim == k / dim) ? 1.0 : 0.0;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? std::atoi(argv[1]) : 2048;
+  const bool rnd = argc > 2 && std::string(argv[2]) == "random";
+  int nbits = 0;
+  while ((1 << nbits) < n) ++nbits;
+  const size_t nn = (size_t)n * n;
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  rocblas_handle h;
+  rocblas_create_handle(&h);
+  rocblas_set_stream(h, st);
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int n_cu = prop.multiProcessorCount;
+  double *A0, *A, *V, *lam, *lref, *e;
+  void* work;
+  rocblas_int* info;
+  CK(hipMalloc(&A0, nn * 8));
+  CK(hipMalloc(&A, nn * 8));
+  CK(hipMalloc(&V, nn * 8));
+  CK(hipMalloc(&lam, n * 8));
+  CK(hipMalloc(&lref, n * 8));
+  CK(hipMalloc(&e, n * 8));
+  CK(hipMalloc(&work, dse::eig2_workspace(n)));
+  CK(hipMalloc(&info, sizeof(rocblas_int)));
+  CK(hipMemsetAsync(A0, 0, nn * 8, st));
+  if (rnd)
+    hipLaunchKernelGGL(k_rand, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st, A0, n, 7u);
+  else
+    hipLaunchKernelGGL(k_fill, dim3((n + 255) / 256), dim3(256), 0, st, A0, n, nbits, 7u);
+  auto reset = [&] {
+    CK(hipMemcpyAsync(A, A0, nn * 8, hipMemcpyDeviceToDevice, st));
+    CK(hipStreamSynchronize(st));
+  };
+  // reference eigenvalues
+  reset();
+  rocsolver_dsyevd(h, rocblas_evect_none, rocblas_fill_lower, n, A, n, lref, e, info);
+  CK(hipStreamSynchronize(st));
+  for (int rep = 0; rep < 2; ++rep) {
+    reset();
+    double t[6];
+    t[0] = now_ms();
+    int rc1 = dse::sy2sb_lower(h, st, n, A, n, work);
+    CK(hipStreamSynchronize(st));
+    t[1] = now_ms();
+    int rc2 = dse::sb2st_lower(st, n, A, n, lam, e, work, n_cu);
+    CK(hipStreamSynchronize(st));
+    t[2] = now_ms();
+    rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, n, info);
+    CK(hipStreamSynchronize(st));
+    t[3] = now_ms();
+    int rc3 = dse::q2_apply(st, n, V, n, work);
+    CK(hipStreamSynchronize(st));
+    t[4] = now_ms();
+    // Q1 via the public two-stage entry's last step: ormtr_lower(offset 32) on the stage-1 reflectors
+    int rc4 = dse::eig2_q1(h, st, n, A, n, V, n, work);
+    CK(hipStreamSynchronize(st));
+    t[5] = now_ms();
+    std::printf("{\"dim\": %d, \"rep\": %d, \"sy2sb_ms\": %.1f, \"sb2st_ms\": %.1f, \"stedc_ms\": %.1f, \"q2_ms\": %.1f, "
+                "\"q1_ms\": %.1f, \"total_ms\": %.1f, \"rc\": [%d, %d, %d, %d]}\n",
+                n, rep, t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[5] - t[0], rc1, rc2, rc3,
+                rc4);
+    std::fflush(stdout);
+  }
+  std::vector<double> a(n), b(n);
+  CK(hipMemcpy(a.data(), lam, n * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(b.data(), lref, n * 8, hipMemcpyDeviceToHost));
+  double dl = 0.0, ml = 0.0;
+  for (int k = 0; k < n; ++k) dl = std::max(dl, std::fabs(a[k] - b[k])), ml = std::max(ml, std::fabs(b[k]));
+  const double one = 1.0, mone = -1.0;
+  rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+  rocblas_ddgmm(h, rocblas_side_right, n, n, V, n, lam, 1, A, n);
+  rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, n, n, n, &one, A0, n, V, n, &mone, A, n);
+  rocblas_int ia = 0;
+  rocblas_idamax(h, (rocblas_int)std::min(nn, (size_t)0x7fffffff), A, 1, &ia);
+  double res = 0.0;
+  CK(hipMemcpy(&res, A + (ia - 1), 8, hipMemcpyDeviceToHost));
+  hipLaunchKernelGGL(k_eye, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st, A, n);
+  rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, n, n, n, &one, V, n, V, n, &mone, A, n);
+  rocblas_idamax(h, (rocblas_int)std::min(nn, (size_t)0x7fffffff), A, 1, &ia);
+  double orth = 0.0;
+  CK(hipMemcpy(&orth, A + (ia - 1), 8, hipMemcpyDeviceToHost));
+  rocblas_int inf = 0;
+  CK(hipMemcpy(&inf, info, sizeof(inf), hipMemcpyDeviceToHost));
+  std::printf("{\"dim\": %d, \"matrix\": \"%s\", \"check\": 1, \"lam_rel\": %.3e, \"resid_rel\": %.3e, \"orth\": %.3e, "
+              "\"info\": %d, \"lam_max\": %.4f, \"workspace_mb\": %.1f}\n",
+              n, rnd ? "random" : "h14-like", dl / ml, std::fabs(res) / ml, std::fabs(orth), inf, ml,
+              dse::eig2_workspace(n) / 1048576.0);
+  return 0;
+}
