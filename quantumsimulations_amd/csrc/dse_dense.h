@@ -94,7 +94,8 @@ int eig_sym_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, d
 // doubles); n_cu: compute units (the chase's workgroups are co-resident)
 size_t eig2_workspace(int n);
 int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work);
-int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu);
+int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu,
+                long long* dbg = nullptr);
 int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work);
 int eig2_q1(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, double* Z, int ldz, void* work);
 int eig_sym_2stage(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,

@@ -53,14 +53,31 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// all co-resident workgroups of the launch reach target (counter monotone within the launch)
+// all co-resident workgroups of the launch reach target (counter monotone within the launch).  The
+// payload crosses in the guide's valid form (MI355X_MICROARCH.md "Valid forms", row 1): sc1 stores
+// and loads, each storing wave's s_waitcnt vmcnt(0) before the barrier, relaxed agent counter.
 __device__ __forceinline__ void grid_sync(int* cnt, int target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    while (__hip_atomic_load(cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
   }
   __syncthreads();
+}
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ptr_rsrc(const void* p, size_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)bytes, 0x00020000);
+}
+constexpr int kBandSc1 = 16;  // aux: sc1 (dse_device.h kSc1)
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int e) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, e * 8, 0, kBandSc1));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int e, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, e * 8, 0, kBandSc1);
 }
 
 // ---- stage 1 ------------------------------------------------------------------------------------
@@ -73,10 +90,13 @@ __global__ void __launch_bounds__(kPanelRows)
 k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
            double* __restrict__ piv, int* __restrict__ cnt) {
   __shared__ double red[kPanelRows / 64][kB];
+  __shared__ double red8[8][kB];
   __shared__ double tot[kB];
   __shared__ double prow[kB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = gridDim.x;
+  const __amdgpu_buffer_rsrc_t prs = ptr_rsrc(part, (size_t)2 * G * (kB + 1) * 8);
+  const __amdgpu_buffer_rsrc_t vrs = ptr_rsrc(piv, (size_t)2 * kB * 8);
   const int r = blockIdx.x * kPanelRows + tid;
   const bool own = r < m;
   double x[kB];
@@ -85,7 +105,7 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
   const int kmax = min(m, kB);
   for (int j = 0; j < kmax; ++j) {
     const int par = j & 1;
-    double* pj = part + ((size_t)par * G + blockIdx.x) * (kB + 1);
+    const int pj = (par * G + blockIdx.x) * (kB + 1);
     // slot j: sum of squares of x_j below row j; slot k > j: sum of x_j x_k below row j
     const bool below = own && r > j;
     double xj = 0.0;
@@ -100,16 +120,31 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
     }
     if (own && r == j) {
 #pragma unroll
-      for (int k = 0; k < kB; ++k) piv[par * kB + k] = x[k];
+      for (int k = 0; k < kB; ++k) bstore(vrs, par * kB + k, x[k]);
     }
     __syncthreads();
-    if (tid < kB && tid >= j) pj[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (tid < kB && tid >= j) bstore(prs, pj + tid, red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
     grid_sync(cnt, (j + 1) * G);
-    if (tid < kB && tid >= j) {
+    {  // the G partials: thread (k, g0) sums g = g0, g0 + 8, ... (G <= 128), then the 8 in fixed order
+      const int k = tid & 31, g0 = tid >> 5;
+      double pv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int g = g0 + 8 * q;
+        pv[q] = (k >= j && g < G) ? bload(prs, (par * G + g) * (kB + 1) + k) : 0.0;
+      }
       double s = 0.0;
-      for (int g = 0; g < G; ++g) s += part[((size_t)par * G + g) * (kB + 1) + tid];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += pv[q];
+      red8[g0][k] = s;
+      if (tid < kB) prow[tid] = tid >= j ? bload(vrs, par * kB + tid) : 0.0;
+    }
+    __syncthreads();
+    if (tid < kB) {
+      double s = 0.0;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s += red8[g][tid];
       tot[tid] = s;
-      prow[tid] = piv[par * kB + tid];
     }
     __syncthreads();
     const double alpha = prow[j], s2 = tot[j];
@@ -153,12 +188,45 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
   }
 }
 
-// Vw (m x k, ld m): the panel's reflectors with their unit diagonal and zeros above
+// Vw (m x kB, ld m) and its row-major copy Vt (Vt[r kB + q]): the panel's reflectors with their
+// unit diagonal, zeros above it and past k
 __global__ void __launch_bounds__(256)
-k_sb_vcopy(const double* __restrict__ P, int lda, int m, int k, double* __restrict__ Vw) {
-  const int r = (int)(blockIdx.x * 256 + threadIdx.x), q = (int)blockIdx.y;  // q < kB: zero past k
+k_sb_vcopy(const double* __restrict__ P, int lda, int m, int k, double* __restrict__ Vw, double* __restrict__ Vt) {
+  const int r = (int)(blockIdx.x * 256 + threadIdx.x);
   if (r >= m) return;
-  Vw[(size_t)q * m + r] = q >= k ? 0.0 : r > q ? P[(size_t)q * lda + r] : (r == q ? 1.0 : 0.0);
+#pragma unroll 4
+  for (int q = 0; q < kB; ++q) {
+    const double v = q >= k ? 0.0 : r > q ? P[(size_t)q * lda + r] : (r == q ? 1.0 : 0.0);
+    Vw[(size_t)q * m + r] = v;
+    Vt[(size_t)r * kB + q] = v;
+  }
+}
+
+// T (kB x kB upper, ld kB) of the panel's block reflector I - V T V^T (LAPACK dlarft, forward,
+// columnwise): T(j, j) = tau_j, T(0:j, j) = -tau_j T(0:j, 0:j) (V^T V)(0:j, j), with V^T V the sum
+// of k_sb_vty's partials (fixed order); one workgroup
+__global__ void __launch_bounds__(kB * kB)
+k_sb_tmat(const double* __restrict__ part, int ng, int k, const double* __restrict__ tau, double* __restrict__ T) {
+  __shared__ double G[kB][kB + 1];
+  __shared__ double Ts[kB][kB + 1];
+  const int e = threadIdx.x, p = e % kB, q = e / kB;
+  double a = 0.0;
+  for (int g = 0; g < ng; ++g) a += part[(size_t)g * kB * kB + e];
+  G[p][q] = a;
+  Ts[p][q] = 0.0;
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    const double tj = tau[j];
+    if (e < j) {
+      double sum = 0.0;
+      for (int c = e; c < j; ++c) sum = fma(Ts[e][c], G[c][j], sum);
+      Ts[e][j] = -tj * sum;
+    } else if (e == j) {
+      Ts[j][j] = tj;
+    }
+    __syncthreads();
+  }
+  T[(size_t)q * kB + p] = (p < k && q < k) ? Ts[p][q] : 0.0;
 }
 
 // ---- stage 1's trailing update on the matrix cores (v_mfma_f64_16x16x4_f64: lane l holds A(l & 15,
@@ -172,49 +240,90 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Y (m x kB, ld m) = A22 V for the symmetric A22 (lower triangle stored, ld lda), V m x kB (ld m).
-// Workgroup = 64-row block I, 4 waves x 16 rows; tiles J <= I as stored, J > I transposed (A_JI^T).
+// Partial Y_I = sum over the column tiles J of chunk blockIdx.y of A22_IJ V_J for the symmetric
+// A22 (lower triangle stored, ld lda): tiles J < I as stored, J > I from the stored A_JI (their
+// columns are contiguous: one 16-B load = two k-steps), J = I and ragged edge tiles element-wise.
+// Wave w takes the chunk's tiles w, w + 4, ..., all 64 x 32 outputs of a tile in its registers;
+// the k-steps of an MFMA pair are columns c = 8 u + 2 (lane >> 4) + e, e = 0, 1, of the tile (any
+// order of the 4 k-slots works when both operands use it).  The waves' sums meet in LDS (fixed
+// order); Yp[(ch kB + q) m + r] holds chunk ch's partial.
+constexpr int kSymmCh = 16;  // column tiles per workgroup
 __global__ void __launch_bounds__(256)
-k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict__ V, double* __restrict__ Y) {
-  __shared__ double T[kT][kTP];
-  __shared__ double Vt[kT][kB + 4];
-  const int I = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, double* __restrict__ Yp) {
+  __shared__ double red[kB][kT + 1];
+  const int I = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lq = lane >> 4;
   const int nbk = (m + kT - 1) / kT;
   const int r0 = I * kT;
-  f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-  for (int J = 0; J < nbk; ++J) {
+  f64x4 acc[4][2];
+#pragma unroll
+  for (int rs = 0; rs < 4; ++rs) acc[rs][0] = acc[rs][1] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int jb = ch * kSymmCh, je = min(nbk, jb + kSymmCh);
+  for (int J = jb + w; J < je; J += 4) {
     const int c0 = J * kT;
-    __syncthreads();
-    // T(r, c) = A(r0 + r, c0 + c) from the lower triangle: stored at column min, row max
-    for (int e = tid; e < kT * kT; e += 256) {
-      const int a = e & 63, b = e >> 6;  // a: fast index
-      int r, c;
-      if (J <= I) r = a, c = b;  // column-major reads of A(r0 + r, c0 + c), rows contiguous
-      else r = b, c = a;         // A(c0 + c, r0 + r) is stored: contiguous in c
-      const int gr = r0 + r, gc = c0 + c;
-      double v = 0.0;
-      if (gr < m && gc < m) v = gr >= gc ? A[(size_t)gc * lda + gr] : A[(size_t)gr * lda + gc];
-      T[r][c] = v;
-    }
-    for (int e = tid; e < kT * kB; e += 256) {
-      const int c = e & 63, k = e >> 6;
-      Vt[c][k] = c0 + c < m ? V[(size_t)k * m + c0 + c] : 0.0;
-    }
-    __syncthreads();
+    double a[4][16], b[2][16];
+    const bool full = J != I && r0 + kT <= m && c0 + kT <= m;
+    if (full && J < I) {
 #pragma unroll
-    for (int kk = 0; kk < kT / 4; ++kk) {
-      const double a = T[16 * w + (lane & 15)][4 * kk + (lane >> 4)];
-      acc0 = mfma64(a, Vt[4 * kk + (lane >> 4)][lane & 15], acc0);
-      acc1 = mfma64(a, Vt[4 * kk + (lane >> 4)][16 + (lane & 15)], acc1);
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int rs = 0; rs < 4; ++rs)
+            a[rs][2 * u + e] = A[(size_t)(c0 + 8 * u + 2 * lq + e) * lda + r0 + 16 * rs + li];
+    } else if (full) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int rs = 0; rs < 4; ++rs) {
+          const double2 v = *reinterpret_cast<const double2*>(A + (size_t)(r0 + 16 * rs + li) * lda + c0 + 8 * u + 2 * lq);
+          a[rs][2 * u] = v.x;
+          a[rs][2 * u + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int rs = 0; rs < 4; ++rs) {
+            const int gr = r0 + 16 * rs + li, gc = c0 + 8 * u + 2 * lq + e;
+            a[rs][2 * u + e] = (gr < m && gc < m) ? (gr >= gc ? A[(size_t)gc * lda + gr] : A[(size_t)gr * lda + gc]) : 0.0;
+          }
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int gc = c0 + 8 * u + 2 * lq + e;
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs) b[cs][2 * u + e] = gc < m ? Vt[(size_t)gc * kB + 16 * cs + li] : 0.0;
+      }
+#pragma unroll
+    for (int st = 0; st < 16; ++st)
+#pragma unroll
+      for (int rs = 0; rs < 4; ++rs)
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs) acc[rs][cs] = mfma64(a[rs][st], b[cs][st], acc[rs][cs]);
   }
+  // D(row (lane >> 4) + 4 x, col lane & 15) of output tile (rs, cs) = Y(16 rs + row, 16 cs + col)
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = r0 + 16 * w + (lane >> 4) + 4 * r;
-    if (row < m) {
-      Y[(size_t)(lane & 15) * m + row] = acc0[r];
-      Y[(size_t)(16 + (lane & 15)) * m + row] = acc1[r];
+      for (int rs = 0; rs < 4; ++rs)
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            double& d = red[16 * cs + li][16 * rs + lq + 4 * x];
+            d = ww == 0 ? acc[rs][cs][x] : d + acc[rs][cs][x];
+          }
     }
+    __syncthreads();
+  }
+  for (int e = tid; e < kB * kT; e += 256) {
+    const int r = e & 63, q = e >> 6;
+    if (r0 + r < m) Yp[((size_t)ch * kB + q) * m + r0 + r] = red[q][r];
   }
 }
 
@@ -229,6 +338,14 @@ k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ V,
   __shared__ double Q[kT][kTP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r0 = I * kT, c0 = J * kT;
+  double old[4][4];  // the A tile, loaded while the operands are staged
+#pragma unroll
+  for (int sc = 0; sc < 4; ++sc)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gc = c0 + 16 * w + (lane >> 4) + 4 * r, gr = r0 + 16 * sc + (lane & 15);
+      old[sc][r] = (gr < m && gc < m && gr >= gc) ? A[(size_t)gc * lda + gr] : 0.0;
+    }
   for (int e = tid; e < kT * kB; e += 256) {
     const int r = e & 63, k = e >> 6;
     const bool ri = r0 + r < m, cj = c0 + r < m;
@@ -252,8 +369,27 @@ k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ V,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int gc = c0 + 16 * w + (lane >> 4) + 4 * r, gr = r0 + 16 * sc + (lane & 15);
-      if (gr < m && gc < m && gr >= gc) A[(size_t)gc * lda + gr] -= acc[sc][r];
+      if (gr < m && gc < m && gr >= gc) A[(size_t)gc * lda + gr] = old[sc][r] - acc[sc][r];
     }
+}
+
+// Y (m x kB, ld m) = the sum of k_sb_symm's nch partials (fixed order), one thread per element
+__global__ void __launch_bounds__(256)
+k_sb_ysum(double* __restrict__ Y, const double* __restrict__ Yp, int nch, int m) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x, mk = (size_t)m * kB;
+  if (e >= mk) return;
+  double a = 0.0;
+  int c = 0;
+  for (; c + 4 <= nch; c += 4) {
+    const double x0 = Yp[(size_t)c * mk + e], x1 = Yp[(size_t)(c + 1) * mk + e];
+    const double x2 = Yp[(size_t)(c + 2) * mk + e], x3 = Yp[(size_t)(c + 3) * mk + e];
+    a += x0;
+    a += x1;
+    a += x2;
+    a += x3;
+  }
+  for (; c < nch; ++c) a += Yp[(size_t)c * mk + e];
+  Y[e] = a;
 }
 
 // Y <- Y T (T kB x kB upper, ld kB) row-wise in place (small: m kB^2 / 2 FMAs; rows in LDS)
@@ -383,7 +519,6 @@ __device__ __forceinline__ double* refl_at(double* refl, const long long* goff, 
 
 // One task (s, t) by one wave, the three 32 x 32 blocks in registers: lane = column j (L, D) or row
 // i (R) of a 16-row / 16-column half h = lane >> 5.  v, w and the annihilated column in LDS.
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t band_rsrc(double* S, int n) {
   const uint64_t a = (uint64_t)S;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
@@ -394,21 +529,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t band_rsrc(double* S, int n) {
 // the guide's valid form (MI355X_MICROARCH.md "Valid forms", row 1, per wave: every load and
 // store of the band sc1, each storing wave's s_waitcnt vmcnt(0) before its sc1 flag store, the
 // consumer wave polls the flag with sc1 loads and then loads)
-constexpr int kBandSc1 = 16;  // aux: sc1 (dse_device.h kSc1)
-__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int e) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, e * 8, 0, kBandSc1));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int e, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, e * 8, 0, kBandSc1);
-}
 
 struct ChaseVec {
   double x[kB];
   double v[kB];
   double w[kB];
+  double Lt[kB][kB + 1];  // L and D between the memory layout (lane = row) and the compute layout
+  double Dt[kB][kB + 1];  // (lane = column); pitch kB + 1: both conflict-free
 };
 
-__device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec& B, double* __restrict__ rf) {
+__device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+
+template <bool DBG>
+__device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec& B, double* __restrict__ rf,
+                           long long* tl) {
   const int lane = threadIdx.x & 63;
   const int j = lane & 31, h = lane >> 5, i0 = 16 * h;
   const int col = t == 0 ? s : s + (t - 1) * kB + 1;
@@ -418,26 +552,39 @@ __device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec
   const int mr = max(0, min(kB, n - r0 - m));
   const __amdgpu_buffer_rsrc_t rs = band_rsrc(S, n);
   double Lc[16], Dc[16], Rr[16];
-  // L(i, j) = A(r0 + i, col + j); D(i, j) = A(r0 + i, r0 + j); R(i, jj) = A(r0 + m + i, r0 + jj)
-  const int eL = (col + j) * kLD + (r0 - col - j) + i0;  // + q
-  const int eD = (r0 + j) * kLD + (i0 - j);              // + q, rows i >= j
-  const int eDu = (r0 + i0) * kLD + (j - i0);            // + q (kLD - 1), rows i < j
-  const int eR = (r0 + i0) * kLD + (m + j - i0);         // + q (kLD - 1)
+  // L(i, j) = A(r0 + i, col + j); D(i, j) = A(r0 + i, r0 + j) (i >= j stored); R(i, jj) =
+  // A(r0 + m + i, r0 + jj).  Memory layout: lane = row i (band column contiguous), load q takes
+  // columns 2 q + h; R is read in its compute layout (lane = row, contiguous already).
+  const int eR = (r0 + i0) * kLD + (m + j - i0);  // + q (kLD - 1)
+  {
+    double Lm[16], Dm[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = 2 * q + h;
+      Lm[q] = (j < m && c < nL) ? bload(rs, (col + c) * kLD + (r0 - col - c) + j) : 0.0;
+      Dm[q] = (j < m && c < m && j >= c) ? bload(rs, (r0 + c) * kLD + j - c) : 0.0;
+      const int jj = i0 + q;
+      Rr[q] = (j < mr && jj < m) ? bload(rs, eR + q * (kLD - 1)) : 0.0;
+    }
+    if constexpr (DBG) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tl[0] = rt_now();
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      B.Lt[j][2 * q + h] = Lm[q];
+      B.Dt[j][2 * q + h] = Dm[q];
+    }
+  }
+  wave_sync();
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int i = i0 + q;
-    Lc[q] = (i < m && j < nL) ? bload(rs, eL + q) : 0.0;
-    double dv = 0.0;
-    if (i < m && j < m) dv = i >= j ? bload(rs, eD + q) : bload(rs, eDu + q * (kLD - 1));
-    Dc[q] = dv;
-    const int jj = i0 + q;
-    Rr[q] = (j < mr && jj < m) ? bload(rs, eR + q * (kLD - 1)) : 0.0;
+    Lc[q] = B.Lt[i][j];
+    Dc[q] = i >= j ? B.Dt[i][j] : B.Dt[j][i];
   }
   // the reflector of L(:, 0)
-  if (j == 0) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) B.x[i0 + q] = Lc[q];
-  }
+  if (lane < kB) B.x[lane] = B.Lt[lane][0];
   wave_sync();
   const double xi = lane < kB ? B.x[lane] : 0.0;
   const double alpha = B.x[0];
@@ -450,6 +597,7 @@ __device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec
   }
   if (lane < kB) B.v[lane] = lane == 0 ? 1.0 : (lane < m ? xi * sc : 0.0);
   wave_sync();
+  if constexpr (DBG) tl[1] = rt_now();
   if (tau != 0.0) {
     double vh[16];
 #pragma unroll
@@ -492,13 +640,24 @@ __device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec
 #pragma unroll
       for (int q = 0; q < 16; ++q) Rr[q] = fma(-z, vh[q], Rr[q]);
     }
+    if constexpr (DBG) tl[2] = rt_now();
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int i = i0 + q;
-      if (i < m && j < nL) bstore(rs, eL + q, Lc[q]);
-      if (i < m && j < m && i >= j) bstore(rs, eD + q, Dc[q]);
       const int jj = i0 + q;
       if (j < mr && jj < m) bstore(rs, eR + q * (kLD - 1), Rr[q]);
+    }
+    wave_sync();  // every lane's reads of Lt / Dt above are done
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      B.Lt[i0 + q][j] = Lc[q];
+      B.Dt[i0 + q][j] = Dc[q];
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = 2 * q + h;
+      if (j < m && c < nL) bstore(rs, (col + c) * kLD + (r0 - col - c) + j, B.Lt[j][c]);
+      if (j < m && c < m && j >= c) bstore(rs, (r0 + c) * kLD + j - c, B.Dt[j][c]);
     }
   }
   if (lane == 0) rf[kB] = tau;
@@ -510,26 +669,53 @@ __device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec
 // sweeps w, w + W, ...; task (s, t) waits until sweep s - 1 has finished task t + 2 (or all its
 // tasks): the strips of (s, t) and (s - 1, t + 3) share no entry (tools/proto_two_stage.py).
 // prog[s] = tasks of sweep s done (zeroed before); relaxed agent-scope (sc1) flag stores and polls.
+// DBG: per worker, the sums of the poll wait, load, compute + store issue and store drain times
+// (100 MHz ticks) and the task count into dbg[5 w ..].
 constexpr int kChaseWG = 4;  // waves per chase workgroup
+template <bool DBG>
 __global__ void __launch_bounds__(64 * kChaseWG)
 k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long long* __restrict__ goff,
-        int* __restrict__ prog) {
+        int* __restrict__ prog, long long* __restrict__ dbg) {
   __shared__ ChaseVec lds[kChaseWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = gridDim.x * kChaseWG, w = blockIdx.x * kChaseWG + wv;
   ChaseVec& B = lds[wv];
+  long long sw = 0, sl = 0, sc = 0, sd = 0, cnt = 0;
   for (int s = w; s < n - 1; s += W) {
     const int nt = chase_tasks(n, s);
     const int ntp = s > 0 ? chase_tasks(n, s - 1) : 0;
     for (int t = 0; t < nt; ++t) {
+      long long t0 = 0, t1 = 0, tls[3] = {0, 0, 0}, t2 = 0;
+      if constexpr (DBG) t0 = rt_now();
       if (s > 0) {
         const int need = min(ntp, t + 3);
         while (__hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
           __builtin_amdgcn_s_sleep(1);
       }
-      chase_task(S, n, s, t, B, refl_at(refl, goff, s, t));
+      if constexpr (DBG) t1 = rt_now();
+      chase_task<DBG>(S, n, s, t, B, refl_at(refl, goff, s, t), tls);
+      const long long tl = tls[0];
+      if constexpr (DBG) t2 = rt_now();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(prog + s, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (DBG) {
+        const long long t3 = rt_now();
+        sw += t1 - t0, sl += tl - t1, sc += t2 - tl, sd += t3 - t2, ++cnt;
+        // per sweep: start (after the wait) and flag times of tasks 0, 1, 2
+        if (lane == 0 && t < 3) dbg[5 * 4096 + 6 * s + 2 * t] = t1, dbg[5 * 4096 + 6 * s + 2 * t + 1] = t3;
+        // every task (n <= 4096): wait start, start, load done, flag at (s nt(0) + t) 4
+        if (lane == 0 && n <= 4096) {
+          long long* q = dbg + 5 * 4096 + 6 * (size_t)n + ((size_t)s * chase_tasks(n, 0) + t) * 4;
+          q[0] = tls[1], q[1] = t1, q[2] = tl, q[3] = t3;
+          q[4 * chase_tasks(n, 0) * (size_t)n] = tls[2];  // second plane: after the updates
+          q[4 * chase_tasks(n, 0) * (size_t)n + 1] = t2;
+        }
+      }
+    }
+  }
+  if constexpr (DBG) {
+    if (lane == 0) {
+      dbg[5 * w] = sw, dbg[5 * w + 1] = sl, dbg[5 * w + 2] = sc, dbg[5 * w + 3] = sd, dbg[5 * w + 4] = cnt;
     }
   }
 }
@@ -565,11 +751,9 @@ k_sb_q2(double* __restrict__ Z, int ldz, int n, const double* __restrict__ refl,
   const int colg = blockIdx.x * 64 + lane;
   const bool live = colg < n;
   double* zc = Z + (size_t)(live ? colg : 0) * ldz;
-  const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)Z >> 32)) << 32) |
-              __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)Z)),
-      0, 0x7fffffff, 0x00020000);
-  const uint32_t cbase = (uint32_t)((size_t)(live ? colg : 0) * ldz);  // element offset of the column
+  // resource based at the workgroup's first column (64 columns < 2^31 bytes)
+  const __amdgpu_buffer_rsrc_t zr = ptr_rsrc(Z + (size_t)blockIdx.x * 64 * ldz, (size_t)64 * ldz * 8);
+  const uint32_t cbase = (uint32_t)((live ? lane : 0) * ldz);  // element offset of the column
   auto zld = [&](int row) -> double {  // sc1: another wave of this CU may have rewritten the line
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, (int)((cbase + (uint32_t)row) * 8u),
                                                                             0, kBandSc1));
@@ -659,6 +843,8 @@ struct Eig2Ws {
   double* T;        // panels x b x b
   double* Vw;       // n x b
   double* Y;        // n x b
+  double* Vt;       // n x b, row-major
+  double* Yp;       // symm partials: chunks x b x n
   double* M;        // b x b
   double* Gm;       // b x b
   double* part;     // 2 x 128 x (b + 1)
@@ -701,6 +887,8 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.T = (double*)take((size_t)panels * kB * kB * 8);
   w.Vw = (double*)take((size_t)n * kB * 8);
   w.Y = (double*)take((size_t)n * kB * 8);
+  w.Vt = (double*)take((size_t)n * kB * 8);
+  w.Yp = (double*)take((size_t)((n / kT + 1 + kSymmCh - 1) / kSymmCh) * kB * n * 8);
   w.M = (double*)take((size_t)kB * kB * 8);
   w.Gm = (double*)take((size_t)kB * kB * 8);
   w.part = (double*)take((size_t)2 * 128 * (kB + 1) * 8);
@@ -738,14 +926,14 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     if (hipGetLastError() != hipSuccess) return -1;
     const int k = std::min(m, kB);
     double* T = ws.T + (size_t)p * kB * kB;
-    if (rocsolver_dlarft(h, rocblas_forward_direction, rocblas_column_wise, m, k, P, lda, ws.tau1 + i, T, kB) !=
-        rocblas_status_success)
-      return -3;
-    hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256, kB), dim3(256), 0, st, P, lda, m, k, ws.Vw);
+    const int nbk = (m + kT - 1) / kT, ng = (m + 255) / 256, nch = (nbk + kSymmCh - 1) / kSymmCh;
+    hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256), dim3(256), 0, st, P, lda, m, k, ws.Vw, ws.Vt);
+    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Vw, m, ws.part2);
+    hipLaunchKernelGGL(k_sb_tmat, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, ws.tau1 + i, T);
     double* A22 = A + (size_t)(i + kB) * lda + i + kB;
-    const int nbk = (m + kT - 1) / kT, ng = (m + 255) / 256;
     // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
-    hipLaunchKernelGGL(k_sb_symm, dim3(nbk), dim3(256), 0, st, A22, lda, m, ws.Vw, ws.Y);
+    hipLaunchKernelGGL(k_sb_symm, dim3(nbk, nch), dim3(256), 0, st, A22, lda, m, ws.Vt, ws.Yp);
+    hipLaunchKernelGGL(k_sb_ysum, dim3((unsigned)(((size_t)m * kB + 255) / 256)), dim3(256), 0, st, ws.Y, ws.Yp, nch, m);
     hipLaunchKernelGGL(k_sb_yt, dim3(ng), dim3(256), 0, st, ws.Y, m, k, T);
     hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Y, m, ws.part2);
     hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
@@ -755,7 +943,8 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu) {
+int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu,
+                long long* dbg) {
   Eig2Ws ws = carve2(work, n);
   std::vector<long long> goff;
   const size_t nrefl = chase_refl_doubles(n, &goff);
@@ -765,7 +954,10 @@ int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, doub
   hipLaunchKernelGGL(k_sb_band, dim3((unsigned)(((size_t)n * kLD + 255) / 256)), dim3(256), 0, st, A, lda, n, ws.S);
   // ~n / (3 b) sweeps run at once: one worker per 2 b columns, at most one workgroup per CU
   const int nwg = std::max(1, std::min(n_cu, (n + 2 * kB * kChaseWG - 1) / (2 * kB * kChaseWG)));
-  hipLaunchKernelGGL(k_sb2st, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog);
+  if (dbg)
+    hipLaunchKernelGGL(k_sb2st<true>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, dbg);
+  else
+    hipLaunchKernelGGL(k_sb2st<false>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, dbg);
   hipLaunchKernelGGL(k_sb_tridiag, dim3((n + 255) / 256), dim3(256), 0, st, ws.S, n, d, e);
   if (hipStreamSynchronize(st) != hipSuccess) return -1;  // goff is host memory until here
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -786,7 +978,7 @@ int eig_sym_2stage(rocblas_handle h, hipStream_t st, int n, double* A, int lda, 
                    double* e, void* work, int* info, int n_cu) {
   int rc = sy2sb_lower(h, st, n, A, lda, work);
   if (rc) return rc;
-  if ((rc = sb2st_lower(st, n, A, lda, lam, e, work, n_cu))) return rc;
+  if ((rc = sb2st_lower(st, n, A, lda, lam, e, work, n_cu, nullptr))) return rc;
   if (rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, ldv, info) != rocblas_status_success) return -8;
   if ((rc = q2_apply(st, n, V, ldv, work))) return rc;
   return eig2_q1(h, st, n, A, lda, V, ldv, work);

@@ -94,6 +94,12 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&e, n * 8));
   CK(hipMalloc(&work, dse::eig2_workspace(n)));
   CK(hipMalloc(&info, sizeof(rocblas_int)));
+  // EIG2_CHASE_DBG=1: the chase's per-worker phase times (k_sb2st<true>)
+  long long* dbg = nullptr;
+  const bool chase_dbg = std::getenv("EIG2_CHASE_DBG") && std::atoi(std::getenv("EIG2_CHASE_DBG"));
+  const size_t ntr = n <= 4096 ? (size_t)n * (1 + (n - 2) / 32) * 8 : 0;
+  const size_t ndbg = (size_t)5 * 4096 + 6 * (size_t)n + ntr;
+  if (chase_dbg) CK(hipMalloc(&dbg, ndbg * 8));
   CK(hipMemsetAsync(A0, 0, nn * 8, st));
   if (rnd)
     hipLaunchKernelGGL(k_rand, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st, A0, n, 7u);
@@ -114,7 +120,7 @@ int main(int argc, char** argv) {
     int rc1 = dse::sy2sb_lower(h, st, n, A, n, work);
     CK(hipStreamSynchronize(st));
     t[1] = now_ms();
-    int rc2 = dse::sb2st_lower(st, n, A, n, lam, e, work, n_cu);
+    int rc2 = dse::sb2st_lower(st, n, A, n, lam, e, work, n_cu, dbg);
     CK(hipStreamSynchronize(st));
     t[2] = now_ms();
     rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, n, info);
@@ -132,6 +138,45 @@ int main(int argc, char** argv) {
                 n, rep, t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[5] - t[0], rc1, rc2, rc3,
                 rc4);
     std::fflush(stdout);
+    if (chase_dbg) {
+      std::vector<long long> h(ndbg, 0);
+      CK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+      double sum[5] = {0, 0, 0, 0, 0};
+      int workers = 0;
+      for (int w = 0; w < 4096; ++w)
+        if (h[5 * w + 4] > 0) {
+          ++workers;
+          for (int q = 0; q < 5; ++q) sum[q] += (double)h[5 * w + q];
+        }
+      // 100 MHz ticks -> us per task
+      std::printf("{\"dim\": %d, \"chase_dbg\": 1, \"workers\": %d, \"tasks\": %.0f, \"us_per_task\": {\"wait\": %.2f, "
+                  "\"load\": %.2f, \"compute_store\": %.2f, \"drain_flag\": %.2f}}\n",
+                  n, workers, sum[4], sum[0] / sum[4] / 100.0, sum[1] / sum[4] / 100.0, sum[2] / sum[4] / 100.0,
+                  sum[3] / sum[4] / 100.0);
+      // critical chain: sweep s starts task 0 after sweep s - 1 flagged task 2
+      double acc[6] = {0, 0, 0, 0, 0, 0};  // busy0, wait1, busy1, wait2, busy2, flag2(s-1) -> start0(s)
+      int cntl = 0;
+      for (int q = 1; q < n - 1; ++q) {
+        const long long* c = &h[5 * 4096 + 6 * q];
+        const long long* p = &h[5 * 4096 + 6 * (q - 1)];
+        if (!c[5] || !p[5]) continue;
+        acc[0] += c[1] - c[0], acc[1] += c[2] - c[1], acc[2] += c[3] - c[2], acc[3] += c[4] - c[3], acc[4] += c[5] - c[4];
+        acc[5] += c[0] - p[5];
+        ++cntl;
+      }
+      std::printf("{\"dim\": %d, \"chase_chain\": 1, \"sweeps\": %d, \"us\": {\"busy0\": %.2f, \"wait1\": %.2f, "
+                  "\"busy1\": %.2f, \"wait2\": %.2f, \"busy2\": %.2f, \"flag2_to_next_start\": %.2f}}\n", n, cntl,
+                  acc[0] / cntl / 100, acc[1] / cntl / 100, acc[2] / cntl / 100, acc[3] / cntl / 100, acc[4] / cntl / 100,
+                  acc[5] / cntl / 100);
+      if (std::getenv("EIG2_CHASE_TRACE") && ntr) {  // every task's 4 times, raw int64, (s nt(0) + t) 4
+        FILE* f = std::fopen(std::getenv("EIG2_CHASE_TRACE"), "wb");
+        if (f) {
+          std::fwrite(&h[5 * 4096 + 6 * (size_t)n], 8, ntr, f);
+          std::fclose(f);
+        }
+      }
+      CK(hipMemset(dbg, 0, ndbg * 8));
+    }
   }
   std::vector<double> a(n), b(n);
   CK(hipMemcpy(a.data(), lam, n * 8, hipMemcpyDeviceToHost));
