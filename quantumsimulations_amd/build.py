@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdse.so")
 SOURCES = ["dse_kernels.hip", "dse_interval.hip", "dse_wht.hip", "dse_small.hip", "dse_dense.hip", "dse_matrix.hip",
-           "dse_sytrd.hip", "dse_span.hip", "dse_real.hip", "dse_runtime.hip", "dse_host.cpp"]
+           "dse_sytrd.hip", "dse_eig2.hip", "dse_span.hip", "dse_real.hip", "dse_runtime.hip", "dse_host.cpp"]
 HEADERS = ["dse_internal.h", "dse_device.h", "dse_wht.h", "dse_small.h", "dse_dense.h"]
 ARCH = os.environ.get("DSE_OFFLOAD_ARCH", "gfx950")
 

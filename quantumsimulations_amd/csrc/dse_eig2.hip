@@ -737,27 +737,22 @@ __global__ void k_sb_tridiag(const double* __restrict__ S, int n, double* __rest
 // In a block, t ascending; the group (block, t)'s reflectors (s descending) act on window rows
 // lo .. lo + 62, lo = s0 + t b + 1, reflector s at window offset s - s0 (compile time).  The next
 // group's records (contiguous, refl_at) are loaded into registers while this group is applied.
-// Waves of one workgroup hand rows over through L2: plain stores, s_waitcnt vmcnt(0), then the LDS
-// progress word; the reader's window loads are sc1 (past the CU's L1).
+// Z is row-major here (Zt, row stride ldt: a window row of the 64 columns is one 512-B load).  Waves
+// of one workgroup hand rows over with a workgroup-scope release fence before the LDS progress
+// word and an acquire fence after the poll (the memory model's own workgroup hand-off).
 constexpr int kQ2Rec = kQ2NB * kRec;             // doubles per group
 constexpr int kQ2PerLane = (kQ2Rec + 63) / 64;    // staging loads per lane
 constexpr int kQ2Waves = 4;
 __global__ void __launch_bounds__(64 * kQ2Waves)
-k_sb_q2(double* __restrict__ Z, int ldz, int n, const double* __restrict__ refl, const long long* __restrict__ goff) {
+k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl, const long long* __restrict__ goff) {
   __shared__ __attribute__((aligned(16))) double rvs[kQ2Waves][kQ2PerLane * 64];
   __shared__ int state[kQ2Waves];  // (block order index) * 65536 + groups done (65535: block done)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* rv = rvs[wv];
   const int colg = blockIdx.x * 64 + lane;
   const bool live = colg < n;
-  double* zc = Z + (size_t)(live ? colg : 0) * ldz;
-  // resource based at the workgroup's first column (64 columns < 2^31 bytes)
-  const __amdgpu_buffer_rsrc_t zr = ptr_rsrc(Z + (size_t)blockIdx.x * 64 * ldz, (size_t)64 * ldz * 8);
-  const uint32_t cbase = (uint32_t)((live ? lane : 0) * ldz);  // element offset of the column
-  auto zld = [&](int row) -> double {  // sc1: another wave of this CU may have rewritten the line
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, (int)((cbase + (uint32_t)row) * 8u),
-                                                                            0, kBandSc1));
-  };
+  double* zc = Zt + (live ? colg : 0);
+  auto zld = [&](int row) -> double { return zc[(size_t)row * ldt]; };
   if (lane == 0) state[wv] = -1;
   __syncthreads();
   const int ns = n - 1;
@@ -772,6 +767,7 @@ k_sb_q2(double* __restrict__ Z, int ldz, int n, const double* __restrict__ refl,
       const int need = (i - 1) * 65536 + min(t + 1, 65535);
       while (__hip_atomic_load(&state[pw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
         __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
     const double* gb = refl + goff[blk];
     double pre[kQ2PerLane];
@@ -820,8 +816,8 @@ k_sb_q2(double* __restrict__ Z, int ldz, int n, const double* __restrict__ refl,
       // slide: rows lo .. lo + b - 1 are final for this block
 #pragma unroll
       for (int r = 0; r < kB; ++r)
-        if (live && lo + r < n) zc[lo + r] = win[r];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (live && lo + r < n) zc[(size_t)(lo + r) * ldt] = win[r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
       for (int r = 0; r < kQ2Win - kB; ++r) win[r] = win[r + kB];
@@ -832,9 +828,27 @@ k_sb_q2(double* __restrict__ Z, int ldz, int n, const double* __restrict__ refl,
     }
 #pragma unroll
     for (int r = 0; r < kQ2Win; ++r)
-      if (live && lo + r < n) zc[lo + r] = win[r];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (live && lo + r < n) zc[(size_t)(lo + r) * ldt] = win[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + 65535, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// B (row-major, ld ldb) = A (column-major, ld lda), n x n; or back (the same map with the roles of
+// the two layouts swapped): 64 x 64 tiles through LDS, reads and writes along contiguous rows
+__global__ void __launch_bounds__(256)
+k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, int ldb, int n) {
+  __shared__ double tile[64][65];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tid = threadIdx.x;
+  const int a = tid & 63, b0 = tid >> 6;
+  for (int b = b0; b < 64; b += 4) {  // column c0 + b of A, rows r0 + a
+    const int r = r0 + a, c = c0 + b;
+    tile[b][a] = (r < n && c < n) ? A[(size_t)c * lda + r] : 0.0;
+  }
+  __syncthreads();
+  for (int b = b0; b < 64; b += 4) {  // row r0 + b of B, columns c0 + a
+    const int r = r0 + b, c = c0 + a;
+    if (r < n && c < n) B[(size_t)r * ldb + c] = tile[a][b];
   }
 }
 
@@ -845,6 +859,7 @@ struct Eig2Ws {
   double* Y;        // n x b
   double* Vt;       // n x b, row-major
   double* Yp;       // symm partials: chunks x b x n
+  double* Zt;       // n x n: Z row-major for the Q2 application
   double* M;        // b x b
   double* Gm;       // b x b
   double* part;     // 2 x 128 x (b + 1)
@@ -888,6 +903,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.Vw = (double*)take((size_t)n * kB * 8);
   w.Y = (double*)take((size_t)n * kB * 8);
   w.Vt = (double*)take((size_t)n * kB * 8);
+  w.Zt = (double*)take((size_t)n * n * 8);
   w.Yp = (double*)take((size_t)((n / kT + 1 + kSymmCh - 1) / kSymmCh) * kB * n * 8);
   w.M = (double*)take((size_t)kB * kB * 8);
   w.Gm = (double*)take((size_t)kB * kB * 8);
@@ -965,7 +981,11 @@ int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, doub
 
 int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
   Eig2Ws ws = carve2(work, n);
-  hipLaunchKernelGGL(k_sb_q2, dim3((n + 63) / 64), dim3(64 * kQ2Waves), 0, st, Z, ldz, n, ws.refl, ws.goff);
+  const dim3 tg((n + 63) / 64, (n + 63) / 64);
+  hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, Z, ldz, ws.Zt, n, n);
+  hipLaunchKernelGGL(k_sb_q2, dim3((n + 63) / 64), dim3(64 * kQ2Waves), 0, st, ws.Zt, n, n, ws.refl, ws.goff);
+  // back: Z(r, c) = Zt[r n + c], i.e. the column-major read of Zt^T
+  hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, ws.Zt, n, Z, ldz, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

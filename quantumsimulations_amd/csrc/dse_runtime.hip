@@ -1355,8 +1355,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "eig_streams") {  // dense engine: large eigendecompositions at a time (1..8)
     if (!(value >= 1 && value <= 8)) return fail(ctx, DSE_ERR_ARG, "eig_streams must be in 1..8");
     ctx->eig_streams = (int)value;
-  } else if (k == "eig_impl") {  // dense engine eigensolver: 0 dsyevd, 1 auto, 2 half-matrix from 2^10
-    if (!(value == 0 || value == 1 || value == 2)) return fail(ctx, DSE_ERR_ARG, "eig_impl must be 0, 1 or 2");
+  } else if (k == "eig_impl") {  // dense engine eigensolver: 0 dsyevd, 1 auto, 2 half-matrix from 2^10,
+                                 // 3 two-stage from 2^10
+    if (!(value >= 0 && value <= 3)) return fail(ctx, DSE_ERR_ARG, "eig_impl must be 0, 1, 2 or 3");
     ctx->eig_impl = (int)value;
   } else if (k == "dense_refine") {  // dense engine: refined eigenvalues + double-double phases
     ctx->dense_refine = value != 0.0;
@@ -1837,6 +1838,10 @@ bool dense_eligible(const HostProblem& P) {
 // 0.46 vs 0.68 s at 2^13, 2.35 vs 4.12 s at 2^14 (profiles/r03/sytrd_probe.jsonl,
 // profiles/r03/ab/sytrd_column_kernels_ab.jsonl)
 constexpr size_t kEigHalfMinDim = 2048;
+// eig_impl 1 from 2^14: eig_sym_2stage (dse_eig2.hip: band reduction, bulge chase, dstedc, Q2, Q1)
+// measured 1.79 s against eig_sym_lower's 2.35 s at 2^14 (profiles/r04/eig2_probe.jsonl); at 2^12
+// 0.19 s against 0.13 s
+constexpr size_t kEig2MinDim = 16384;
 
 // Seconds of device time, by the measured rates: the Chebyshev propagator at ~15 TF/s of its
 // algorithmic FP64 work (the N = 14 bench runs at 16.5 chip-level) with ~25 extra terms per
@@ -1920,7 +1925,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
   };
   std::unique_ptr<DevArena> scr_arena;
   std::vector<EigScratch> scr;
-  size_t scr_dim = 0;
+  size_t scr_dim = 0, scr_work = 0;
   size_t idx = 0;
   while (idx < order.size()) {
     // ---- round: jobs while 60% of the free memory lasts (at least one register) ----
@@ -2029,24 +2034,29 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     // half-matrix eigensolver scratch per solver stream: a copy of H' (the solver's A; V receives
     // the eigenvectors), tau and the tridiagonalisation workspace, sized for the round's largest
     // such register; kept across rounds
-    size_t half_min = ctx->eig_impl == 2 ? 1024 : ctx->eig_impl == 1 ? kEigHalfMinDim : SIZE_MAX;
-    size_t half_dim = 0;
+    size_t half_min = ctx->eig_impl == 2 ? 1024 : ctx->eig_impl == 1 ? kEigHalfMinDim : ctx->eig_impl == 3 ? 1024 : SIZE_MAX;
+    const size_t two_min = ctx->eig_impl == 3 ? 1024 : ctx->eig_impl == 1 ? kEig2MinDim : SIZE_MAX;
+    size_t half_dim = 0, two_dim = 0;
     for (const Task& T : tasks)
-      if (T.i >= 0 && T.j->dim >= half_min) half_dim = std::max(half_dim, T.j->dim);
-    if (half_dim > scr_dim) {
+      if (T.i >= 0 && T.j->dim >= half_min) {
+        half_dim = std::max(half_dim, T.j->dim);
+        if (T.j->dim >= two_min) two_dim = std::max(two_dim, T.j->dim);
+      }
+    const size_t work_b = std::max(sytrd_workspace((int)half_dim), two_dim ? eig2_workspace((int)two_dim) : (size_t)0);
+    if (half_dim > scr_dim || work_b > scr_work) {
       scr.clear();
       scr_arena.reset(new DevArena);
-      scr_dim = 0;
+      scr_dim = 0, scr_work = 0;
       for (int w = 0; w < K; ++w) {
         EigScratch S;
         S.A = scr_arena->get<double>(half_dim * half_dim);
         S.tau = scr_arena->get<double>(half_dim);
-        S.work = scr_arena->get<double>(sytrd_workspace((int)half_dim) / sizeof(double) + 1);
+        S.work = scr_arena->get<double>(work_b / sizeof(double) + 1);
         if (!S.A || !S.tau || !S.work) break;
         scr.push_back(S);
       }
       if ((int)scr.size() == K) {
-        scr_dim = half_dim;
+        scr_dim = half_dim, scr_work = work_b;
       } else {  // no room beside the round's jobs: dsyevd in place
         (void)hipGetLastError();
         scr.clear();
@@ -2079,7 +2089,10 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           double* Vi = J.V + J.dim * J.dim * i;
           werr[w] = hipMemcpyAsync(scr[w].A, Vi, J.dim * J.dim * sizeof(double), hipMemcpyDeviceToDevice,
                                    ctx->eig_st[w]);
-          if (werr[w] == hipSuccess)
+          if (werr[w] == hipSuccess && J.dim >= two_min)
+            wrc[w] = eig_sym_2stage(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
+                                    J.E + J.dim * i, scr[w].work, J.info + i, ctx->n_cu);
+          else if (werr[w] == hipSuccess)
             wrc[w] = eig_sym_lower(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
                                    J.E + J.dim * i, scr[w].tau, scr[w].work, J.info + i);
         } else if (T.i >= 0) {

@@ -16,6 +16,9 @@ output time exact from one GEMM (rocBLAS dgemm) and the observable pass.
 * the half-matrix eigensolver (csrc/dse_sytrd.hip, option eig_impl): config 2 through it at dim 4096
   against the exact fixture (1e-10) and against rocSOLVER dsyevd (1e-11); an N = 13 register (dim
   8192, its default range) against dsyevd on a 1 s grid, to the phase drift of eigenvalue rounding
+* the two-stage eigensolver (csrc/dse_eig2.hip, eig_impl 3; eig_impl 1 takes it from 2^14, so the
+  N = 14 tests above run it): config 2 at dim 4096 against the exact fixture and dsyevd, and an
+  N = 13 register against dsyevd as for the half-matrix one
 """
 import json
 import os
@@ -191,3 +194,29 @@ def test_half_eigensolver_n13_matches_dsyevd(engine):
     tol = 1e-11 + 1e-8 * t
     assert np.all(np.abs(hm - ev) <= tol), np.max(np.abs(hm - ev) - tol)
     assert np.max(np.abs(s_hm[0] - s_ev[0])) < 1e-8
+
+
+def test_two_stage_eigensolver_config2_matches_exact_and_dsyevd(engine, golden):
+    tr = golden("traces_n12.npz")
+    t = tr["t"]
+    p = sweep_point_params(11, 50000.0, "center_on", float(t[-1]), len(t))
+    ts, st, s_ts = _evolve(engine, [p], t, 2, eig_impl=3)
+    ev, _, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st["dense_problems"] == 1
+    for j, k in enumerate(OBS):
+        err = np.max(np.abs(ts[0, j] - tr[f"exact_{k}"]))
+        assert err < 1e-10, (k, err)
+    assert np.max(np.abs(ts - ev)) < 1e-11
+    assert np.max(np.abs(s_ts[0] - s_ev[0])) < 1e-11
+
+
+def test_two_stage_eigensolver_n13_matches_dsyevd(engine):
+    t = np.linspace(0.0, 1.0, 2001)
+    p = sweep_point_params(12, 100e3, "center_on", 1.0, 2001)
+    ts, st, s_ts = _evolve(engine, [p], t, 2, eig_impl=3)
+    ev, _, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st["dense_problems"] == 1
+    np.testing.assert_allclose(ts[:, 6], 1.0, atol=1e-10)
+    tol = 1e-11 + 1e-8 * t  # as for the half-matrix solver: eigenvalue rounding drift
+    assert np.all(np.abs(ts - ev) <= tol), np.max(np.abs(ts - ev) - tol)
+    assert np.max(np.abs(s_ts[0] - s_ev[0])) < 1e-8
