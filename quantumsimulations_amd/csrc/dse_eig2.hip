@@ -85,10 +85,11 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int e, double v
 // Householder QR of the m x kB panel P (column-major, ld lda) in place, LAPACK dgeqr2's layout
 // (R on and above the diagonal, v below it with v_0 = 1 implied, tau[j]).  Thread = row; the
 // workgroups are co-resident (gridDim.x <= CUs), one grid barrier per column.  part: 2 x gridDim.x
-// x (kB + 1) doubles, piv: 2 x kB doubles, cnt zeroed before the launch.
+// x (kB + 1) doubles, piv: 2 x kB doubles; cnt counts on from base (zeroed once per reduction, the
+// host adds each panel's kB x gridDim.x arrivals to base).
 __global__ void __launch_bounds__(kPanelRows)
 k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
-           double* __restrict__ piv, int* __restrict__ cnt) {
+           double* __restrict__ piv, int* __restrict__ cnt, int base) {
   __shared__ double red[kPanelRows / 64][kB];
   __shared__ double red8[8][kB];
   __shared__ double tot[kB];
@@ -124,7 +125,7 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
     }
     __syncthreads();
     if (tid < kB && tid >= j) bstore(prs, pj + tid, red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
-    grid_sync(cnt, (j + 1) * G);
+    grid_sync(cnt, base + (j + 1) * G);
     {  // the G partials: thread (k, g0) sums g = g0, g0 + 8, ... (G <= 128), then the 8 in fixed order
       const int k = tid & 31, g0 = tid >> 5;
       double pv[16];
@@ -328,49 +329,76 @@ k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict
 }
 
 // A22 (lower, ld lda) -= V W^T + W V^T on the 64 x 64 tiles on and below the diagonal: D' = Q P^T
-// with P = [V_I | W_I], Q = [W_J | V_J] (64 x 2 kB each); D'(c, r) -= into A(I 64 + r, J 64 + c),
-// lanes along r (contiguous rows of column-major A)
+// with P = [V_I | W_I], Q = [W_J | V_J] (64 x 2 kB each), D'(c, r) -= into A(I 64 + r, J 64 + c).
+// Operands straight from the row-major copies Vt, Wt (16-B loads: k = 8 u + 2 (lane >> 4) + e, as
+// k_sb_symm); wave w takes columns c of subtile w, the A tile's loads issued first.
 __global__ void __launch_bounds__(256)
-k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ V, const double* __restrict__ W) {
+k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, const double* __restrict__ Wt) {
   const int I = blockIdx.x, J = blockIdx.y;
   if (J > I) return;
-  __shared__ double P[kT][kTP];
-  __shared__ double Q[kT][kTP];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lq = lane >> 4;
   const int r0 = I * kT, c0 = J * kT;
-  double old[4][4];  // the A tile, loaded while the operands are staged
+  double old[4][4];
 #pragma unroll
   for (int sc = 0; sc < 4; ++sc)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gc = c0 + 16 * w + (lane >> 4) + 4 * r, gr = r0 + 16 * sc + (lane & 15);
-      old[sc][r] = (gr < m && gc < m && gr >= gc) ? A[(size_t)gc * lda + gr] : 0.0;
+    for (int x = 0; x < 4; ++x) {
+      const int gc = c0 + 16 * w + lq + 4 * x, gr = r0 + 16 * sc + li;
+      old[sc][x] = (gr < m && gc < m && gr >= gc) ? A[(size_t)gc * lda + gr] : 0.0;
     }
-  for (int e = tid; e < kT * kB; e += 256) {
-    const int r = e & 63, k = e >> 6;
-    const bool ri = r0 + r < m, cj = c0 + r < m;
-    P[r][k] = ri ? V[(size_t)k * m + r0 + r] : 0.0;
-    P[r][kB + k] = ri ? W[(size_t)k * m + r0 + r] : 0.0;
-    Q[r][k] = cj ? W[(size_t)k * m + c0 + r] : 0.0;
-    Q[r][kB + k] = cj ? V[(size_t)k * m + c0 + r] : 0.0;
+  const int qc = c0 + 16 * w + li;
+  double qa[16];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const double* src = u < 4 ? Wt : Vt;
+    double2 v = double2{0.0, 0.0};
+    if (qc < m) v = *reinterpret_cast<const double2*>(src + (size_t)qc * kB + (u & 3) * 8 + 2 * lq);
+    qa[2 * u] = v.x;
+    qa[2 * u + 1] = v.y;
   }
-  __syncthreads();
   f64x4 acc[4];
 #pragma unroll
-  for (int sc = 0; sc < 4; ++sc) acc[sc] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int sc = 0; sc < 4; ++sc) {
+    const int pr = r0 + 16 * sc + li;
+    double pb[16];
 #pragma unroll
-  for (int kk = 0; kk < 2 * kB / 4; ++kk) {
-    const double a = Q[16 * w + (lane & 15)][4 * kk + (lane >> 4)];
+    for (int u = 0; u < 8; ++u) {
+      const double* src = u < 4 ? Vt : Wt;
+      double2 v = double2{0.0, 0.0};
+      if (pr < m) v = *reinterpret_cast<const double2*>(src + (size_t)pr * kB + (u & 3) * 8 + 2 * lq);
+      pb[2 * u] = v.x;
+      pb[2 * u + 1] = v.y;
+    }
+    acc[sc] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int sc = 0; sc < 4; ++sc) acc[sc] = mfma64(a, P[16 * sc + (lane & 15)][4 * kk + (lane >> 4)], acc[sc]);
+    for (int st = 0; st < 16; ++st) acc[sc] = mfma64(qa[st], pb[st], acc[sc]);
   }
 #pragma unroll
   for (int sc = 0; sc < 4; ++sc)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gc = c0 + 16 * w + (lane >> 4) + 4 * r, gr = r0 + 16 * sc + (lane & 15);
-      if (gr < m && gc < m && gr >= gc) A[(size_t)gc * lda + gr] = old[sc][r] - acc[sc][r];
+    for (int x = 0; x < 4; ++x) {
+      const int gc = c0 + 16 * w + lq + 4 * x, gr = r0 + 16 * sc + li;
+      if (gr < m && gc < m && gr >= gc) A[(size_t)gc * lda + gr] = old[sc][x] - acc[sc][x];
     }
+}
+
+// Y <- Y T (T kB x kB upper, ld kB): one thread per output Y(r, q) (32 per row, the row's Y in
+// L1), T in LDS
+__global__ void __launch_bounds__(256)
+k_sb_yt2(const double* __restrict__ Y, double* __restrict__ Yo, int m, int k, const double* __restrict__ T) {
+  __shared__ double Ts[kB][kB + 1];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < kB * kB; e += 256) {
+    const int i = e % kB, j = e / kB;
+    Ts[i][j] = (i < k && j < k && i <= j) ? T[(size_t)j * kB + i] : 0.0;
+  }
+  __syncthreads();
+  const int r = blockIdx.x * 8 + (tid >> 5), q = tid & 31;  // lanes: q fast within a row
+  if (r >= m) return;
+  double a = 0.0;
+#pragma unroll 8
+  for (int p = 0; p < kB; ++p) a = fma(Y[(size_t)p * m + r], Ts[p][q], a);
+  Yo[(size_t)q * m + r] = q < k ? a : 0.0;
 }
 
 // Y (m x kB, ld m) = the sum of k_sb_symm's nch partials (fixed order), one thread per element
@@ -390,26 +418,6 @@ k_sb_ysum(double* __restrict__ Y, const double* __restrict__ Yp, int nch, int m)
   }
   for (; c < nch; ++c) a += Yp[(size_t)c * mk + e];
   Y[e] = a;
-}
-
-// Y <- Y T (T kB x kB upper, ld kB) row-wise in place (small: m kB^2 / 2 FMAs; rows in LDS)
-__global__ void __launch_bounds__(256)
-k_sb_yt(double* __restrict__ Y, int m, int k, const double* __restrict__ T) {
-  __shared__ double Ts[kB][kB + 1];
-  __shared__ double Ys[kB][256 + 1];
-  const int tid = threadIdx.x, r = blockIdx.x * 256 + tid;
-  for (int e = tid; e < kB * kB; e += 256) {
-    const int i = e % kB, j = e / kB;
-    Ts[i][j] = (i < k && j < k && i <= j) ? T[(size_t)j * kB + i] : 0.0;
-  }
-  for (int q = 0; q < kB; ++q) Ys[q][tid] = (r < m && q < k) ? Y[(size_t)q * m + r] : 0.0;
-  __syncthreads();
-  if (r >= m) return;
-  for (int q = 0; q < k; ++q) {
-    double a = 0.0;
-    for (int p = 0; p <= q; ++p) a = fma(Ys[p][tid], Ts[p][q], a);
-    Y[(size_t)q * m + r] = a;
-  }
 }
 
 // part[g] (kB x kB, column-major) = V_g^T Y_g over the 256-row chunk g, on the matrix cores
@@ -476,7 +484,8 @@ k_sb_gm(const double* __restrict__ part, int ng, int k, const double* __restrict
 
 // W = Y2 - V Gm / 2 row-wise in place (into Y)
 __global__ void __launch_bounds__(256)
-k_sb_w(double* __restrict__ Y, const double* __restrict__ V, int m, int k, const double* __restrict__ Gm) {
+k_sb_w(double* __restrict__ Y, const double* __restrict__ V, int m, int k, const double* __restrict__ Gm,
+       double* __restrict__ Wt) {
   __shared__ double Gs[kB][kB];
   const int tid = threadIdx.x, r = blockIdx.x * 256 + tid;
   for (int e = tid; e < kB * kB; e += 256) Gs[e % kB][e / kB] = Gm[e];
@@ -491,7 +500,9 @@ k_sb_w(double* __restrict__ Y, const double* __restrict__ V, int m, int k, const
     double a = 0.0;
 #pragma unroll
     for (int p = 0; p < kB; ++p) a = fma(v[p], Gs[p][q], a);
-    Y[(size_t)q * m + r] -= 0.5 * a;
+    const double wv = Y[(size_t)q * m + r] - 0.5 * a;
+    Y[(size_t)q * m + r] = wv;
+    Wt[(size_t)r * kB + q] = wv;
   }
 }
 
@@ -751,8 +762,19 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
   double* rv = rvs[wv];
   const int colg = blockIdx.x * 64 + lane;
   const bool live = colg < n;
-  double* zc = Zt + (live ? colg : 0);
-  auto zld = [&](int row) -> double { return zc[(size_t)row * ldt]; };
+  // Zt through a buffer resource at the workgroup's first column: rows past n and columns past n
+  // take an out-of-range offset (loads read 0, stores are dropped), so no row is a branch
+  const size_t zbytes = ((size_t)n * ldt - (size_t)blockIdx.x * 64) * 8;
+  const __amdgpu_buffer_rsrc_t zr = ptr_rsrc(Zt + (size_t)blockIdx.x * 64, std::min<size_t>(zbytes, 0xfffffff0u));
+  auto zoff = [&](int row) -> uint32_t {
+    return (live && row < n) ? ((uint32_t)row * (uint32_t)ldt + (uint32_t)lane) * 8u : 0xffffffffu;
+  };
+  auto zld = [&](int row) -> double {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, zoff(row), 0, 0));
+  };
+  auto zst = [&](int row, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), zr, zoff(row), 0, 0);
+  };
   if (lane == 0) state[wv] = -1;
   __syncthreads();
   const int ns = n - 1;
@@ -780,8 +802,16 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
     int lo = s0 + 1;
     wait_prev(0);
 #pragma unroll
-    for (int r = 0; r < kQ2Win; ++r) win[r] = (live && lo + r < n) ? zld(lo + r) : 0.0;
+    for (int r = 0; r < kQ2Win; ++r) win[r] = zld(lo + r);
     for (int t = 0; t < T0; ++t) {
+      // the rows group t + 1 adds (lo + kQ2Win ..), loaded while group t is applied: block i - 1
+      // has stored them once its group t + 1 is flagged
+      double nxt[kB];
+      if (t + 1 < T0) {
+        wait_prev(t + 1);
+#pragma unroll
+        for (int r = 0; r < kB; ++r) nxt[r] = zld(lo + kQ2Win + r);
+      }
 #pragma unroll
       for (int q = 0; q < kQ2PerLane; ++q) rv[q * 64 + lane] = pre[q];
       __builtin_amdgcn_wave_barrier();
@@ -794,44 +824,72 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
           pre[q] = e < kQ2Rec ? g[e] : 0.0;
         }
       }
+      // reflectors u and u - 1 together: both dot products on the same window, then
+      // g2 = tau2 (d2 - g1 c) with c = v_{u-1}[1:] . v_u[:-1] (record slot kB + 1, k_sb_q2c)
 #pragma unroll
-      for (int u = kQ2NB - 1; u >= 0; --u) {
-        const double* r = rv + u * kRec;
-        const double tau = r[kB];
-        if (tau == 0.0) continue;  // uniform
-        double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+      for (int u = kQ2NB - 1; u >= 1; u -= 2) {
+        const double* r1 = rv + u * kRec;
+        const double* r2 = rv + (u - 1) * kRec;
+        const double tau1 = r1[kB], tau2 = r2[kB];
+        if (tau1 == 0.0 && tau2 == 0.0) continue;  // uniform
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
 #pragma unroll
         for (int k = 0; k < kB; k += 4) {
-          d0 = fma(r[k], win[u + k], d0);
-          d1 = fma(r[k + 1], win[u + k + 1], d1);
-          d2 = fma(r[k + 2], win[u + k + 2], d2);
-          d3 = fma(r[k + 3], win[u + k + 3], d3);
+          a0 = fma(r1[k], win[u + k], a0);
+          b0 = fma(r2[k], win[u - 1 + k], b0);
+          a1 = fma(r1[k + 1], win[u + k + 1], a1);
+          b1 = fma(r2[k + 1], win[u + k], b1);
+          a2 = fma(r1[k + 2], win[u + k + 2], a2);
+          b2 = fma(r2[k + 2], win[u + k + 1], b2);
+          a3 = fma(r1[k + 3], win[u + k + 3], a3);
+          b3 = fma(r2[k + 3], win[u + k + 2], b3);
         }
-        const double g = tau * ((d0 + d1) + (d2 + d3));
+        const double g1 = tau1 * ((a0 + a1) + (a2 + a3));
+        const double g2 = tau2 * (((b0 + b1) + (b2 + b3)) - g1 * r1[kB + 1]);
 #pragma unroll
-        for (int k = 0; k < kB; ++k) win[u + k] = fma(-g, r[k], win[u + k]);
+        for (int k = 0; k < kB; ++k) win[u + k] = fma(-g1, r1[k], win[u + k]);
+#pragma unroll
+        for (int k = 0; k < kB; ++k) win[u - 1 + k] = fma(-g2, r2[k], win[u - 1 + k]);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      // slide: rows lo .. lo + b - 1 are final for this block
+      // group t - 1's rows (stored one group ago) are released now, their stores long complete
+      if (t > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      // rows lo .. lo + b - 1 are final for this block
 #pragma unroll
-      for (int r = 0; r < kB; ++r)
-        if (live && lo + r < n) zc[(size_t)(lo + r) * ldt] = win[r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int r = 0; r < kB; ++r) zst(lo + r, win[r]);
+      if (t + 1 < T0) {
 #pragma unroll
-      for (int r = 0; r < kQ2Win - kB; ++r) win[r] = win[r + kB];
-      lo += kB;
-      if (t + 1 < T0) wait_prev(t + 1);
+        for (int r = 0; r < kQ2Win - kB; ++r) win[r] = win[r + kB];
 #pragma unroll
-      for (int r = kQ2Win - kB; r < kQ2Win; ++r) win[r] = (live && lo + r < n) ? zld(lo + r) : 0.0;
+        for (int r = 0; r < kB; ++r) win[kQ2Win - kB + r] = nxt[r];
+        lo += kB;
+      }
     }
 #pragma unroll
-    for (int r = 0; r < kQ2Win; ++r)
-      if (live && lo + r < n) zc[(size_t)(lo + r) * ldt] = win[r];
+    for (int r = kB; r < kQ2Win; ++r) zst(lo + r, win[r]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + 65535, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+}
+
+// slot kB + 1 of record u >= 1 of each group: c = v_{u-1}[1:kB] . v_u[0:kB-1] (the coupling of the
+// pair k_sb_q2 applies together; 0 for u = 0)
+__global__ void __launch_bounds__(256)
+k_sb_q2c(double* __restrict__ refl, size_t nrec) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nrec) return;
+  double c = 0.0;
+  if (e % kQ2NB != 0) {
+    const double* a = refl + e * kRec;
+    const double* p = a - kRec;
+#pragma unroll
+    for (int k = 0; k < kB - 1; ++k) c = fma(p[k + 1], a[k], c);
+  }
+  refl[e * kRec + kB + 1] = c;
 }
 
 // B (row-major, ld ldb) = A (column-major, ld lda), n x n; or back (the same map with the roles of
@@ -858,6 +916,7 @@ struct Eig2Ws {
   double* Vw;       // n x b
   double* Y;        // n x b
   double* Vt;       // n x b, row-major
+  double* Wt;       // n x b, row-major
   double* Yp;       // symm partials: chunks x b x n
   double* Zt;       // n x n: Z row-major for the Q2 application
   double* M;        // b x b
@@ -903,6 +962,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.Vw = (double*)take((size_t)n * kB * 8);
   w.Y = (double*)take((size_t)n * kB * 8);
   w.Vt = (double*)take((size_t)n * kB * 8);
+  w.Wt = (double*)take((size_t)n * kB * 8);
   w.Zt = (double*)take((size_t)n * n * 8);
   w.Yp = (double*)take((size_t)((n / kT + 1 + kSymmCh - 1) / kSymmCh) * kB * n * 8);
   w.M = (double*)take((size_t)kB * kB * 8);
@@ -931,14 +991,16 @@ size_t eig2_workspace(int n) {
 int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work) {
   Eig2Ws ws = carve2(work, n);
   if (hipMemsetAsync(ws.tau1, 0, (size_t)n * 8, st) != hipSuccess) return -1;
-  int p = 0;
+  if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
+  int p = 0, cbase = 0;
   for (int i = 0; i < n - kB - 1; i += kB, ++p) {
     const int m = n - i - kB;
     double* P = A + (size_t)i * lda + i + kB;
     const int G = (m + kPanelRows - 1) / kPanelRows;
     if (G > 128) return -2;
-    if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, st, P, lda, m, ws.tau1 + i, ws.part, ws.piv, ws.cnt);
+    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, st, P, lda, m, ws.tau1 + i, ws.part, ws.piv, ws.cnt,
+                       cbase);
+    cbase += kB * G;
     if (hipGetLastError() != hipSuccess) return -1;
     const int k = std::min(m, kB);
     double* T = ws.T + (size_t)p * kB * kB;
@@ -950,11 +1012,11 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
     hipLaunchKernelGGL(k_sb_symm, dim3(nbk, nch), dim3(256), 0, st, A22, lda, m, ws.Vt, ws.Yp);
     hipLaunchKernelGGL(k_sb_ysum, dim3((unsigned)(((size_t)m * kB + 255) / 256)), dim3(256), 0, st, ws.Y, ws.Yp, nch, m);
-    hipLaunchKernelGGL(k_sb_yt, dim3(ng), dim3(256), 0, st, ws.Y, m, k, T);
-    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Y, m, ws.part2);
+    hipLaunchKernelGGL(k_sb_yt2, dim3((m + 7) / 8), dim3(256), 0, st, ws.Y, ws.Yp, m, k, T);
+    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Yp, m, ws.part2);
     hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
-    hipLaunchKernelGGL(k_sb_w, dim3(ng), dim3(256), 0, st, ws.Y, ws.Vw, m, k, ws.Gm);
-    hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, ws.Vw, ws.Y);
+    hipLaunchKernelGGL(k_sb_w, dim3(ng), dim3(256), 0, st, ws.Yp, ws.Vw, m, k, ws.Gm, ws.Wt);
+    hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, ws.Vt, ws.Wt);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -982,6 +1044,8 @@ int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, doub
 int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
   Eig2Ws ws = carve2(work, n);
   const dim3 tg((n + 63) / 64, (n + 63) / 64);
+  const size_t nrec = chase_refl_doubles(n) / kRec;
+  hipLaunchKernelGGL(k_sb_q2c, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, st, ws.refl, nrec);
   hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, Z, ldz, ws.Zt, n, n);
   hipLaunchKernelGGL(k_sb_q2, dim3((n + 63) / 64), dim3(64 * kQ2Waves), 0, st, ws.Zt, n, n, ws.refl, ws.goff);
   // back: Z(r, c) = Zt[r n + c], i.e. the column-major read of Zt^T
