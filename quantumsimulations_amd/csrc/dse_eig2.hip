@@ -329,11 +329,13 @@ k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict
 }
 
 // A22 (lower, ld lda) -= V W^T + W V^T on the 64 x 64 tiles on and below the diagonal: D' = Q P^T
-// with P = [V_I | W_I], Q = [W_J | V_J] (64 x 2 kB each), D'(c, r) -= into A(I 64 + r, J 64 + c).
+// with P = [V_I | W_I], Q = [W_J | V_J] (64 x 2 kB each), D'(c, r) -= into A(I 64 + r, J 64 + c)
+// for the columns cmin <= c < cmax of A22.
 // Operands straight from the row-major copies Vt, Wt (16-B loads: k = 8 u + 2 (lane >> 4) + e, as
 // k_sb_symm); wave w takes columns c of subtile w, the A tile's loads issued first.
 __global__ void __launch_bounds__(256)
-k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, const double* __restrict__ Wt) {
+k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, const double* __restrict__ Wt,
+           int cmin, int cmax) {
   const int I = blockIdx.x, J = blockIdx.y;
   if (J > I) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lq = lane >> 4;
@@ -344,7 +346,7 @@ k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int gc = c0 + 16 * w + lq + 4 * x, gr = r0 + 16 * sc + li;
-      old[sc][x] = (gr < m && gc < m && gr >= gc) ? A[(size_t)gc * lda + gr] : 0.0;
+      old[sc][x] = (gr < m && gc < cmax && gc >= cmin && gr >= gc) ? A[(size_t)gc * lda + gr] : 0.0;
     }
   const int qc = c0 + 16 * w + li;
   double qa[16];
@@ -378,7 +380,7 @@ k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int gc = c0 + 16 * w + lq + 4 * x, gr = r0 + 16 * sc + li;
-      if (gr < m && gc < m && gr >= gc) A[(size_t)gc * lda + gr] = old[sc][x] - acc[sc][x];
+      if (gr < m && gc < cmax && gc >= cmin && gr >= gc) A[(size_t)gc * lda + gr] = old[sc][x] - acc[sc][x];
     }
 }
 
@@ -754,33 +756,41 @@ __global__ void k_sb_tridiag(const double* __restrict__ S, int n, double* __rest
 constexpr int kQ2Rec = kQ2NB * kRec;             // doubles per group
 constexpr int kQ2PerLane = (kQ2Rec + 63) / 64;    // staging loads per lane
 constexpr int kQ2Waves = 4;
-__global__ void __launch_bounds__(64 * kQ2Waves)
+// NC columns per lane (64 NC per workgroup): each reflector value read from LDS serves 2 NC FMAs.
+// PF: group t + 1's new rows are loaded under group t (and released one group late); PAIR: two
+// reflectors per step (both dot products on one window).
+// DMA: the group records go global -> LDS directly (global_load_lds, 16 B per lane, double-buffered,
+// no staging registers); W waves per workgroup.
+constexpr int kQ2Dma = (kQ2Rec * 8 + 1023) / 1024;  // 1-KiB copies per group
+template <int NC, bool PF, bool PAIR, bool DMA, int W>
+__global__ void __launch_bounds__(64 * W)
 k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl, const long long* __restrict__ goff) {
-  __shared__ __attribute__((aligned(16))) double rvs[kQ2Waves][kQ2PerLane * 64];
-  __shared__ int state[kQ2Waves];  // (block order index) * 65536 + groups done (65535: block done)
+  constexpr int kBuf = DMA ? 2 * kQ2Dma * 128 : kQ2PerLane * 64;  // doubles per wave
+  __shared__ __attribute__((aligned(16))) double rvs[W][kBuf];
+  __shared__ int state[W];  // (block order index) * 65536 + groups done (65535: block done)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* rv = rvs[wv];
-  const int colg = blockIdx.x * 64 + lane;
-  const bool live = colg < n;
+  const int col0 = blockIdx.x * 64 * NC;
   // Zt through a buffer resource at the workgroup's first column: rows past n and columns past n
   // take an out-of-range offset (loads read 0, stores are dropped), so no row is a branch
-  const size_t zbytes = ((size_t)n * ldt - (size_t)blockIdx.x * 64) * 8;
-  const __amdgpu_buffer_rsrc_t zr = ptr_rsrc(Zt + (size_t)blockIdx.x * 64, std::min<size_t>(zbytes, 0xfffffff0u));
-  auto zoff = [&](int row) -> uint32_t {
-    return (live && row < n) ? ((uint32_t)row * (uint32_t)ldt + (uint32_t)lane) * 8u : 0xffffffffu;
+  const size_t zbytes = ((size_t)n * ldt - (size_t)col0) * 8;
+  const __amdgpu_buffer_rsrc_t zr = ptr_rsrc(Zt + (size_t)col0, std::min<size_t>(zbytes, 0xfffffff0u));
+  auto zoff = [&](int row, int c) -> uint32_t {
+    const int cl = lane + 64 * c;
+    return (col0 + cl < n && row < n) ? ((uint32_t)row * (uint32_t)ldt + (uint32_t)cl) * 8u : 0xffffffffu;
   };
-  auto zld = [&](int row) -> double {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, zoff(row), 0, 0));
+  auto zld = [&](int row, int c) -> double {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(zr, zoff(row, c), 0, 0));
   };
-  auto zst = [&](int row, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), zr, zoff(row), 0, 0);
+  auto zst = [&](int row, int c, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), zr, zoff(row, c), 0, 0);
   };
   if (lane == 0) state[wv] = -1;
   __syncthreads();
   const int ns = n - 1;
   const int nblk = (ns + kQ2NB - 1) / kQ2NB;
-  const int pw = (wv + kQ2Waves - 1) % kQ2Waves;  // the wave of the previous block
-  for (int i = wv; i < nblk; i += kQ2Waves) {
+  const int pw = (wv + W - 1) % W;  // the wave of the previous block
+  for (int i = wv; i < nblk; i += W) {
     const int blk = nblk - 1 - i;
     const int s0 = blk * kQ2NB;
     const int T0 = chase_tasks(n, s0);
@@ -792,85 +802,178 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
     const double* gb = refl + goff[blk];
-    double pre[kQ2PerLane];
+    double pre[DMA ? 1 : kQ2PerLane];
+    auto dma = [&](int t) {  // group t's records into buffer t & 1
+      const char* src = reinterpret_cast<const char*>(gb + (size_t)t * kQ2Rec) + lane * 16;
+      double* dst = rv + (t & 1) * kQ2Dma * 128;
 #pragma unroll
-    for (int q = 0; q < kQ2PerLane; ++q) {
-      const int e = q * 64 + lane;
-      pre[q] = e < kQ2Rec ? gb[e] : 0.0;
+      for (int q = 0; q < kQ2Dma; ++q)
+        __builtin_amdgcn_global_load_lds(src + q * 1024, (__attribute__((address_space(3))) void*)(dst + q * 128), 16, 0, 0);
+    };
+    if constexpr (DMA) {
+      dma(0);
+    } else {
+#pragma unroll
+      for (int q = 0; q < kQ2PerLane; ++q) {
+        const int e = q * 64 + lane;
+        pre[q] = e < kQ2Rec ? gb[e] : 0.0;
+      }
     }
-    double win[kQ2Win];
+    double win[NC][kQ2Win];
     int lo = s0 + 1;
     wait_prev(0);
 #pragma unroll
-    for (int r = 0; r < kQ2Win; ++r) win[r] = zld(lo + r);
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < kQ2Win; ++r) win[c][r] = zld(lo + r, c);
     for (int t = 0; t < T0; ++t) {
-      // the rows group t + 1 adds (lo + kQ2Win ..), loaded while group t is applied: block i - 1
-      // has stored them once its group t + 1 is flagged
+      // NC = 1: the rows group t + 1 adds (lo + kQ2Win ..), loaded while group t is applied: block
+      // i - 1 has stored them once its group t + 1 is flagged
       double nxt[kB];
-      if (t + 1 < T0) {
-        wait_prev(t + 1);
+      if constexpr (PF) {
+        if (t + 1 < T0) {
+          wait_prev(t + 1);
 #pragma unroll
-        for (int r = 0; r < kB; ++r) nxt[r] = zld(lo + kQ2Win + r);
-      }
-#pragma unroll
-      for (int q = 0; q < kQ2PerLane; ++q) rv[q * 64 + lane] = pre[q];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (t + 1 < T0) {
-        const double* g = gb + (size_t)(t + 1) * kQ2Rec;
-#pragma unroll
-        for (int q = 0; q < kQ2PerLane; ++q) {
-          const int e = q * 64 + lane;
-          pre[q] = e < kQ2Rec ? g[e] : 0.0;
+          for (int r = 0; r < kB; ++r) nxt[r] = zld(lo + kQ2Win + r, 0);
         }
       }
+      const double* rg = rv;  // this group's records
+      if constexpr (DMA) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // group t's copy (and the window rows) landed
+        __builtin_amdgcn_wave_barrier();
+        rg = rv + (t & 1) * kQ2Dma * 128;
+        if (t + 1 < T0) dma(t + 1);
+      } else {
+#pragma unroll
+        for (int q = 0; q < kQ2PerLane; ++q) rv[q * 64 + lane] = pre[q];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (t + 1 < T0) {
+          const double* g = gb + (size_t)(t + 1) * kQ2Rec;
+#pragma unroll
+          for (int q = 0; q < kQ2PerLane; ++q) {
+            const int e = q * 64 + lane;
+            pre[q] = e < kQ2Rec ? g[e] : 0.0;
+          }
+        }
+      }
+      if constexpr (!PAIR) {  // one reflector at a time
+#pragma unroll
+        for (int u = kQ2NB - 1; u >= 0; --u) {
+          const double* r = rg + u * kRec;
+          const double tau = r[kB];
+          if (tau == 0.0) continue;  // uniform
+          double d[NC][4];
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int x = 0; x < 4; ++x) d[c][x] = 0.0;
+#pragma unroll
+          for (int k = 0; k < kB; k += 4)
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+              const double p = r[k + x];
+#pragma unroll
+              for (int c = 0; c < NC; ++c) d[c][x] = fma(p, win[c][u + k + x], d[c][x]);
+            }
+          double g[NC];
+#pragma unroll
+          for (int c = 0; c < NC; ++c) g[c] = tau * ((d[c][0] + d[c][1]) + (d[c][2] + d[c][3]));
+#pragma unroll
+          for (int k = 0; k < kB; ++k) {
+            const double p = r[k];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) win[c][u + k] = fma(-g[c], p, win[c][u + k]);
+          }
+        }
+      } else {
       // reflectors u and u - 1 together: both dot products on the same window, then
       // g2 = tau2 (d2 - g1 c) with c = v_{u-1}[1:] . v_u[:-1] (record slot kB + 1, k_sb_q2c)
 #pragma unroll
       for (int u = kQ2NB - 1; u >= 1; u -= 2) {
-        const double* r1 = rv + u * kRec;
-        const double* r2 = rv + (u - 1) * kRec;
+        const double* r1 = rg + u * kRec;
+        const double* r2 = rg + (u - 1) * kRec;
         const double tau1 = r1[kB], tau2 = r2[kB];
         if (tau1 == 0.0 && tau2 == 0.0) continue;  // uniform
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+        double a[NC][4], b[NC][4];
 #pragma unroll
-        for (int k = 0; k < kB; k += 4) {
-          a0 = fma(r1[k], win[u + k], a0);
-          b0 = fma(r2[k], win[u - 1 + k], b0);
-          a1 = fma(r1[k + 1], win[u + k + 1], a1);
-          b1 = fma(r2[k + 1], win[u + k], b1);
-          a2 = fma(r1[k + 2], win[u + k + 2], a2);
-          b2 = fma(r2[k + 2], win[u + k + 1], b2);
-          a3 = fma(r1[k + 3], win[u + k + 3], a3);
-          b3 = fma(r2[k + 3], win[u + k + 2], b3);
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) a[c][x] = b[c][x] = 0.0;
+#pragma unroll
+        for (int k = 0; k < kB; k += 4)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const double p1 = r1[k + x], p2 = r2[k + x];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              a[c][x] = fma(p1, win[c][u + k + x], a[c][x]);
+              b[c][x] = fma(p2, win[c][u - 1 + k + x], b[c][x]);
+            }
+          }
+        const double cpl = r1[kB + 1];
+        double g1[NC], g2[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          g1[c] = tau1 * ((a[c][0] + a[c][1]) + (a[c][2] + a[c][3]));
+          g2[c] = tau2 * (((b[c][0] + b[c][1]) + (b[c][2] + b[c][3])) - g1[c] * cpl);
         }
-        const double g1 = tau1 * ((a0 + a1) + (a2 + a3));
-        const double g2 = tau2 * (((b0 + b1) + (b2 + b3)) - g1 * r1[kB + 1]);
 #pragma unroll
-        for (int k = 0; k < kB; ++k) win[u + k] = fma(-g1, r1[k], win[u + k]);
+        for (int k = 0; k < kB; ++k) {
+          const double p1 = r1[k];
 #pragma unroll
-        for (int k = 0; k < kB; ++k) win[u - 1 + k] = fma(-g2, r2[k], win[u - 1 + k]);
+          for (int c = 0; c < NC; ++c) win[c][u + k] = fma(-g1[c], p1, win[c][u + k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          const double p2 = r2[k];
+#pragma unroll
+          for (int c = 0; c < NC; ++c) win[c][u - 1 + k] = fma(-g2[c], p2, win[c][u - 1 + k]);
+        }
+      }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      // group t - 1's rows (stored one group ago) are released now, their stores long complete
-      if (t > 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if constexpr (PF) {
+        // group t - 1's rows (stored one group ago) are released now, their stores long complete
+        if (t > 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0)
+            __hip_atomic_store(&state[wv], i * 65536 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       // rows lo .. lo + b - 1 are final for this block
 #pragma unroll
-      for (int r = 0; r < kB; ++r) zst(lo + r, win[r]);
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < kB; ++r) zst(lo + r, c, win[c][r]);
+      if constexpr (!PF) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0)
+          __hip_atomic_store(&state[wv], i * 65536 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       if (t + 1 < T0) {
 #pragma unroll
-        for (int r = 0; r < kQ2Win - kB; ++r) win[r] = win[r + kB];
+        for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int r = 0; r < kB; ++r) win[kQ2Win - kB + r] = nxt[r];
+          for (int r = 0; r < kQ2Win - kB; ++r) win[c][r] = win[c][r + kB];
+        if constexpr (PF) {
+#pragma unroll
+          for (int r = 0; r < kB; ++r) win[0][kQ2Win - kB + r] = nxt[r];
+        } else {
+          wait_prev(t + 1);
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int r = 0; r < kB; ++r) win[c][kQ2Win - kB + r] = zld(lo + kQ2Win + r, c);
+        }
         lo += kB;
       }
     }
 #pragma unroll
-    for (int r = kB; r < kQ2Win; ++r) zst(lo + r, win[r]);
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = kB; r < kQ2Win; ++r) zst(lo + r, c, win[c][r]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_store(&state[wv], i * 65536 + 65535, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
@@ -910,12 +1013,19 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
   }
 }
 
+// k_sb_q2 variant (set_eig2_q2_variant; 2^14, profiles/r04/eig2_q2_variants.txt): 0 one
+// reflector at a time, rows loaded after each group (346 ms); 1 pairs + the next rows under the
+// group (361); 2 two columns per lane (649); 3 pairs (357); 4 = 0 with the records copied global ->
+// LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default)
+int g_q2_variant = 5;
+
 struct Eig2Ws {
   double* tau1;     // n: stage-1 reflectors (zero where none)
   double* T;        // panels x b x b
-  double* Vw;       // n x b
+  double* Vw2[2];   // n x b, by panel parity
+  double* Vt2[2];   // n x b, row-major, by panel parity
+  double* part2v;   // V^T V partials (the side stream's)
   double* Y;        // n x b
-  double* Vt;       // n x b, row-major
   double* Wt;       // n x b, row-major
   double* Yp;       // symm partials: chunks x b x n
   double* Zt;       // n x n: Z row-major for the Q2 application
@@ -959,9 +1069,12 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   Eig2Ws w;
   w.tau1 = (double*)take((size_t)n * 8);
   w.T = (double*)take((size_t)panels * kB * kB * 8);
-  w.Vw = (double*)take((size_t)n * kB * 8);
+  for (int q = 0; q < 2; ++q) {
+    w.Vw2[q] = (double*)take((size_t)n * kB * 8);
+    w.Vt2[q] = (double*)take((size_t)n * kB * 8);
+  }
+  w.part2v = (double*)take(((size_t)n / 256 + 2) * kB * kB * 8);
   w.Y = (double*)take((size_t)n * kB * 8);
-  w.Vt = (double*)take((size_t)n * kB * 8);
   w.Wt = (double*)take((size_t)n * kB * 8);
   w.Zt = (double*)take((size_t)n * n * 8);
   w.Yp = (double*)take((size_t)((n / kT + 1 + kSymmCh - 1) / kSymmCh) * kB * n * 8);
@@ -982,43 +1095,80 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
 
 }  // namespace
 
+void set_eig2_q2_variant(int v) { g_q2_variant = v; }
+
 size_t eig2_workspace(int n) {
   size_t b = 0;
   carve2(nullptr, n, &b);
   return b;
 }
 
+// Panel p + 1's QR (and its V copies, V^T V, T) runs on a second stream under panel p's trailing
+// update: the update first rewrites A22's first kB columns (the next panel and its diagonal block),
+// then the rest while the panel is factored; V, its copies and the V^T V partials are double-buffered
+// by panel parity.
 int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work) {
+  (void)h;
   Eig2Ws ws = carve2(work, n);
   if (hipMemsetAsync(ws.tau1, 0, (size_t)n * 8, st) != hipSuccess) return -1;
   if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
-  int p = 0, cbase = 0;
-  for (int i = 0; i < n - kB - 1; i += kB, ++p) {
-    const int m = n - i - kB;
+  hipStream_t s2 = nullptr;
+  hipEvent_t evS = nullptr, evP = nullptr;
+  if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&evS, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&evP, hipEventDisableTiming) != hipSuccess)
+    return -1;
+  int cbase = 0;
+  // the panel at column i: QR, V copies, V^T V partials, T, on stream q
+  auto factor = [&](int i, int p, hipStream_t q) -> int {
+    const int m = n - i - kB, par = p & 1;
     double* P = A + (size_t)i * lda + i + kB;
-    const int G = (m + kPanelRows - 1) / kPanelRows;
+    const int G = (m + kPanelRows - 1) / kPanelRows, ng = (m + 255) / 256, k = std::min(m, kB);
     if (G > 128) return -2;
-    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, st, P, lda, m, ws.tau1 + i, ws.part, ws.piv, ws.cnt,
+    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, q, P, lda, m, ws.tau1 + i, ws.part, ws.piv, ws.cnt,
                        cbase);
     cbase += kB * G;
-    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256), dim3(256), 0, q, P, lda, m, k, ws.Vw2[par], ws.Vt2[par]);
+    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, q, ws.Vw2[par], ws.Vw2[par], m, ws.part2v);
+    hipLaunchKernelGGL(k_sb_tmat, dim3(1), dim3(kB * kB), 0, q, ws.part2v, ng, k, ws.tau1 + i,
+                       ws.T + (size_t)p * kB * kB);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  };
+  int rc = 0, p = 0;
+  const int last = n - kB - 1;  // panels at i < last
+  if (last > 0) rc = factor(0, 0, st);
+  for (int i = 0; i < last && rc == 0; i += kB, ++p) {
+    const int m = n - i - kB, par = p & 1;
     const int k = std::min(m, kB);
-    double* T = ws.T + (size_t)p * kB * kB;
+    const double* T = ws.T + (size_t)p * kB * kB;
+    const double* Vw = ws.Vw2[par];
+    const double* Vt = ws.Vt2[par];
     const int nbk = (m + kT - 1) / kT, ng = (m + 255) / 256, nch = (nbk + kSymmCh - 1) / kSymmCh;
-    hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256), dim3(256), 0, st, P, lda, m, k, ws.Vw, ws.Vt);
-    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Vw, m, ws.part2);
-    hipLaunchKernelGGL(k_sb_tmat, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, ws.tau1 + i, T);
+    if (p > 0 && hipStreamWaitEvent(st, evP, 0) != hipSuccess) rc = -1;
     double* A22 = A + (size_t)(i + kB) * lda + i + kB;
     // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
-    hipLaunchKernelGGL(k_sb_symm, dim3(nbk, nch), dim3(256), 0, st, A22, lda, m, ws.Vt, ws.Yp);
+    hipLaunchKernelGGL(k_sb_symm, dim3(nbk, nch), dim3(256), 0, st, A22, lda, m, Vt, ws.Yp);
     hipLaunchKernelGGL(k_sb_ysum, dim3((unsigned)(((size_t)m * kB + 255) / 256)), dim3(256), 0, st, ws.Y, ws.Yp, nch, m);
     hipLaunchKernelGGL(k_sb_yt2, dim3((m + 7) / 8), dim3(256), 0, st, ws.Y, ws.Yp, m, k, T);
-    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, ws.Vw, ws.Yp, m, ws.part2);
+    hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, Vw, ws.Yp, m, ws.part2);
     hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
-    hipLaunchKernelGGL(k_sb_w, dim3(ng), dim3(256), 0, st, ws.Yp, ws.Vw, m, k, ws.Gm, ws.Wt);
-    hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, ws.Vt, ws.Wt);
+    hipLaunchKernelGGL(k_sb_w, dim3(ng), dim3(256), 0, st, ws.Yp, Vw, m, k, ws.Gm, ws.Wt);
+    if (i + kB < last) {
+      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, 1), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, kB);
+      if (hipEventRecord(evS, st) != hipSuccess || hipStreamWaitEvent(s2, evS, 0) != hipSuccess) rc = -1;
+      if (rc == 0) rc = factor(i + kB, p + 1, s2);
+      if (rc == 0 && hipEventRecord(evP, s2) != hipSuccess) rc = -1;
+      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, kB, m);
+    } else {
+      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, m);
+    }
   }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  if (hipGetLastError() != hipSuccess && rc == 0) rc = -1;
+  (void)hipStreamSynchronize(s2);
+  (void)hipEventDestroy(evS);
+  (void)hipEventDestroy(evP);
+  (void)hipStreamDestroy(s2);
+  return rc;
 }
 
 int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu,
@@ -1047,7 +1197,15 @@ int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
   const size_t nrec = chase_refl_doubles(n) / kRec;
   hipLaunchKernelGGL(k_sb_q2c, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, st, ws.refl, nrec);
   hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, Z, ldz, ws.Zt, n, n);
-  hipLaunchKernelGGL(k_sb_q2, dim3((n + 63) / 64), dim3(64 * kQ2Waves), 0, st, ws.Zt, n, n, ws.refl, ws.goff);
+  const dim3 g1((n + 63) / 64), blk(64 * kQ2Waves);
+  switch (g_q2_variant) {
+    case 1: hipLaunchKernelGGL((k_sb_q2<1, true, true, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 2: hipLaunchKernelGGL((k_sb_q2<2, false, false, false, 4>), dim3((n + 127) / 128), blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 3: hipLaunchKernelGGL((k_sb_q2<1, false, true, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 4: hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 5: hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 8>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    default: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+  }
   // back: Z(r, c) = Zt[r n + c], i.e. the column-major read of Zt^T
   hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, ws.Zt, n, Z, ldz, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
