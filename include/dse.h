@@ -175,7 +175,7 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "dense"        dense eigen-propagator: 0 off, 1 by cost model (default), 2 always
  *          "eig_streams"  dense engine: eigendecompositions of registers of >= 2^10 amplitudes
  *                         run this many at a time, one stream and rocBLAS handle each, 1..8
- *                         (default 2)
+ *                         (default 3)
  *          "eig_impl"     dense engine eigensolver: 0 rocSOLVER dsyevd; 1 (default) for
  *                         registers of >= 2^11 amplitudes a tridiagonalisation (the half-matrix
  *                         one of dse_sytrd.hip from 2^13, rocSOLVER's below), rocSOLVER dstedc

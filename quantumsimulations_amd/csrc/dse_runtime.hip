@@ -264,9 +264,10 @@ struct dse_ctx {
   hipStream_t dense_stream = nullptr;
   rocblas_handle blas = nullptr;
   // dense engine: registers of >= 2^10 amplitudes are diagonalised up to eig_streams at a time (one
-  // host thread, stream and rocBLAS handle each; option "eig_streams", default 2: measured 0.88 of
-  // the one-by-one time per solve at 2^14, 0.81 at 2^13, profiles/r03/eig_concurrency_*.jsonl)
-  int eig_streams = 2;
+  // host thread, stream and rocBLAS handle each; option "eig_streams", default 3: one N = 14 point
+  // of the 30 s grid (two 2^14 registers through the two-stage solver, one 2^13) 4.54 / 4.00 / 3.75 /
+  // 3.87 s with 1 / 2 / 3 / 4 streams, profiles/r04/eig_streams_point_2stage.jsonl)
+  int eig_streams = 3;
   // dense engine eigensolver: 0 rocSOLVER dsyevd at every size; 1 eig_sym_lower (dse_sytrd.hip: the
   // half-matrix tridiagonalisation from 2^13, rocSOLVER dstedc, the blocked back-transformation)
   // from kEigHalfMinDim amplitudes, dsyevd below; 2 eig_sym_lower from 2^10 (tests)
@@ -1858,9 +1859,10 @@ bool dense_cheaper(const HostProblem& P, const double* t, int n_t, bool half_eig
   const double alpha = 0.5 * (P.e_max - P.e_min);
   const double terms = alpha * (t[n_t - 1] - t[0]) + 25.0 * (n_t - 1);
   const double cheb = terms * dim * (P.flops_per_amp > 0 ? P.flops_per_amp : 300.0) / 15e12;
-  const double eig = half_eig && dim >= (double)kEigHalfMinDim
-                         ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
-                         : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
+  double eig = half_eig && dim >= (double)kEigHalfMinDim
+                   ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
+                   : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
+  if (half_eig && dim >= (double)kEig2MinDim) eig *= 0.66;  // two-stage: 1.55 vs 2.35 s at 2^14
   const double dense = eig + 4.0 * dim * dim * n_t / 40e12 + (double)n_t * dim * P.n_local * 32.0 / 2e12;
   return dense < cheb;
 }
