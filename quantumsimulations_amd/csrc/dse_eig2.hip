@@ -733,6 +733,167 @@ k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long lon
   }
 }
 
+// The chase with the next task's operands prefetched (round 4, default).  Task (s, t)'s R block is
+// its next task's L block: it stays in registers (stored there, as L), so a task loads only D and R,
+// and it loads them during the previous task, once sweep s - 1's task t + 1 is done (prog[s - 1] >=
+// t + 2: D_t and R_t are then final but for R_t(b-1, b-1)).  That one element is the annihilated
+// column's head of task (s - 1, t + 2) (its L(0, 0) = beta): the producer publishes beta in the
+// mailbox mb[(s - 1) MT + t + 2] as soon as it has it and never stores the element; the consumer
+// polls the mailbox (8-B sc1, sentinel all-ones) instead of waiting for the whole task.  So task
+// (s, t) waits for (s - 1, t + 1) complete + beta of (s - 1, t + 2) (was: (s - 1, t + 2) complete).
+__global__ void __launch_bounds__(64 * kChaseWG)
+k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long long* __restrict__ goff,
+           int* __restrict__ prog, unsigned long long* __restrict__ mb, int MT) {
+  __shared__ ChaseVec lds[kChaseWG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int W = gridDim.x * kChaseWG, w = blockIdx.x * kChaseWG + wv;
+  const int j = lane & 31, h = lane >> 5, i0 = 16 * h;
+  ChaseVec& B = lds[wv];
+  const __amdgpu_buffer_rsrc_t rs = band_rsrc(S, n);
+  for (int s = w; s < n - 1; s += W) {
+    const int nt = chase_tasks(n, s);
+    const int ntp = s > 0 ? chase_tasks(n, s - 1) : 0;
+    auto wait_prog = [&](int need) {
+      if (s > 0)
+        while (__hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+          __builtin_amdgcn_s_sleep(1);
+    };
+    double Lcar[16], Dm[16], Rm[16];  // carried L (R layout: lane = row), D (memory layout), R
+    auto load_dr = [&](int t) {
+      const int r0 = t == 0 ? s + 1 : s + t * kB + 1;
+      const int m = min(kB, n - r0), mr = max(0, min(kB, n - r0 - m));
+      const int eR = (r0 + i0) * kLD + (m + j - i0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = 2 * q + h, jj = i0 + q;
+        Dm[q] = (j < m && c < m && j >= c) ? bload(rs, (r0 + c) * kLD + j - c) : 0.0;
+        Rm[q] = (j < mr && jj < m) ? bload(rs, eR + q * (kLD - 1)) : 0.0;
+      }
+    };
+    wait_prog(min(ntp, 2));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) Lcar[q] = 0.0;
+    double L0 = (j < min(kB, n - s - 1) && h == 0) ? bload(rs, s * kLD + 1 + j) : 0.0;  // L_0 = A(s + 1 + j, s)
+    load_dr(0);
+    for (int t = 0; t < nt; ++t) {
+      const int col = t == 0 ? s : s + (t - 1) * kB + 1;
+      const int r0 = t == 0 ? s + 1 : s + t * kB + 1;
+      const int m = min(kB, n - r0);
+      const int nL = t == 0 ? 1 : kB;
+      const int mr = max(0, min(kB, n - r0 - m));
+      double* rf = refl_at(refl, goff, s, t);
+      // L and D into LDS (memory layout: lane = row j)
+      if (t == 0) {
+        if (h == 0) B.Lt[j][0] = L0;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) B.Lt[j][i0 + q] = Lcar[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) B.Dt[j][2 * q + h] = Dm[q];
+      // R(b-1, b-1) from task (s - 1, t + 2)
+      if (s > 0 && mr == kB) {
+        unsigned long long bits;
+        while ((bits = __hip_atomic_load(mb + (size_t)(s - 1) * MT + t + 2, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT)) == ~0ull)
+          __builtin_amdgcn_s_sleep(1);
+        if (j == kB - 1 && h == 1) Rm[15] = __builtin_bit_cast(double, bits);
+      }
+      wave_sync();
+      double Lc[16], Dc[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + q;
+        Lc[q] = (t == 0 && j > 0) ? 0.0 : B.Lt[i][j];
+        Dc[q] = i >= j ? B.Dt[i][j] : B.Dt[j][i];
+      }
+      if (lane < kB) B.x[lane] = B.Lt[lane][0];
+      wave_sync();
+      const double xi = lane < kB ? B.x[lane] : 0.0;
+      const double alpha = B.x[0];
+      const double s2 = wave_sum((lane >= 1 && lane < m) ? xi * xi : 0.0);
+      double beta = alpha, tau = 0.0, sc = 0.0;
+      if (s2 != 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + s2), alpha);
+        tau = (beta - alpha) / beta;
+        sc = 1.0 / (alpha - beta);
+      }
+      // L(0, 0)'s new value goes to the consumer (s + 1, t - 2) now
+      if (t >= 2 && lane == 0)
+        __hip_atomic_store(mb + (size_t)s * MT + t, __builtin_bit_cast(unsigned long long, beta), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < kB) B.v[lane] = lane == 0 ? 1.0 : (lane < m ? xi * sc : 0.0);
+      wave_sync();
+      if (tau != 0.0) {
+        double vh[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) vh[q] = B.v[i0 + q];
+        const double vj = B.v[j];
+        {  // L <- H L (column 0 becomes beta e1)
+          double p = 0.0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) p = fma(vh[q], Lc[q], p);
+          const double wl = tau * (p + __shfl_xor(p, 32, 64));
+          if (j == 0) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Lc[q] = (h == 0 && q == 0) ? beta : 0.0;
+          } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Lc[q] = fma(-wl, vh[q], Lc[q]);
+          }
+        }
+        {  // D <- H D H
+          double p = 0.0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) p = fma(vh[q], Dc[q], p);
+          const double y = p + __shfl_xor(p, 32, 64);
+          const double K = wave_sum(lane < kB ? vj * y : 0.0);
+          const double wj = tau * y - 0.5 * tau * tau * K * vj;
+          if (lane < kB) B.w[lane] = wj;
+          wave_sync();
+#pragma unroll
+          for (int q = 0; q < 16; ++q) Dc[q] -= vh[q] * wj + B.w[i0 + q] * vj;
+        }
+        {  // R <- R H (lane = row j)
+          double p = 0.0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) p = fma(vh[q], Rm[q], p);
+          const double z = tau * (p + __shfl_xor(p, 32, 64));
+#pragma unroll
+          for (int q = 0; q < 16; ++q) Rm[q] = fma(-z, vh[q], Rm[q]);
+        }
+      }
+      // stores: L always (a carried L is only in registers), but L(0, 0) from t = 2 on (the
+      // consumer's); D when changed; R stays in registers (the next task's L)
+      wave_sync();  // every lane's reads of Lt / Dt above are done
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        B.Lt[i0 + q][j] = Lc[q];
+        B.Dt[i0 + q][j] = Dc[q];
+      }
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = 2 * q + h;
+        if (j < m && c < nL && !(t >= 2 && j == 0 && c == 0))
+          bstore(rs, (col + c) * kLD + (r0 - col - c) + j, B.Lt[j][c]);
+        if (tau != 0.0 && j < m && c < m && j >= c) bstore(rs, (r0 + c) * kLD + j - c, B.Dt[j][c]);
+      }
+      if (lane == 0) rf[kB] = tau;
+      if (lane < kB) rf[lane] = B.v[lane];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(prog + s, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1 < nt) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Lcar[q] = Rm[q];
+        wait_prog(min(ntp, t + 3));
+        load_dr(t + 1);
+      }
+      wave_sync();
+    }
+  }
+}
+
 // d, e of the tridiagonal from the band
 __global__ void k_sb_tridiag(const double* __restrict__ S, int n, double* __restrict__ d, double* __restrict__ e) {
   const int c = (int)(blockIdx.x * 256 + threadIdx.x);
@@ -1018,6 +1179,8 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
 // group (361); 2 two columns per lane (649); 3 pairs (357); 4 = 0 with the records copied global ->
 // LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default)
 int g_q2_variant = 5;
+// the chase: 0 k_sb2st (waits for (s - 1, t + 2) complete), 1 k_sb2st_pf (default)
+int g_chase_variant = 1;
 
 struct Eig2Ws {
   double* tau1;     // n: stage-1 reflectors (zero where none)
@@ -1039,6 +1202,7 @@ struct Eig2Ws {
   double* orm;      // ormtr_lower workspace
   long long* goff;  // n / kQ2NB + 1: group-major reflector offsets per block of sweeps
   int* prog;        // n
+  unsigned long long* mb;  // n x (chase_tasks(n, 0) + 1): the chase's mailboxes
   int* cnt;         // 1
 };
 
@@ -1088,6 +1252,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.orm = (double*)take(sytrd_workspace(n));
   w.goff = (long long*)take(((size_t)n / kQ2NB + 2) * 8);
   w.prog = (int*)take((size_t)n * 4);
+  w.mb = (unsigned long long*)take((size_t)n * (chase_tasks(n, 0) + 1) * 8);
   w.cnt = (int*)take(256);
   if (bytes) *bytes = off;
   return w;
@@ -1096,6 +1261,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
 }  // namespace
 
 void set_eig2_q2_variant(int v) { g_q2_variant = v; }
+void set_eig2_chase_variant(int v) { g_chase_variant = v; }
 
 size_t eig2_workspace(int n) {
   size_t b = 0;
@@ -1184,8 +1350,13 @@ int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, doub
   const int nwg = std::max(1, std::min(n_cu, (n + 2 * kB * kChaseWG - 1) / (2 * kB * kChaseWG)));
   if (dbg)
     hipLaunchKernelGGL(k_sb2st<true>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, dbg);
-  else
+  else if (g_chase_variant == 0)
     hipLaunchKernelGGL(k_sb2st<false>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, dbg);
+  else {
+    const int MT = chase_tasks(n, 0) + 1;
+    if (hipMemsetAsync(ws.mb, 0xff, (size_t)n * MT * 8, st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_sb2st_pf, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb, MT);
+  }
   hipLaunchKernelGGL(k_sb_tridiag, dim3((n + 255) / 256), dim3(256), 0, st, ws.S, n, d, e);
   if (hipStreamSynchronize(st) != hipSuccess) return -1;  // goff is host memory until here
   return hipGetLastError() == hipSuccess ? 0 : -1;
