@@ -53,19 +53,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// all co-resident workgroups of the launch reach target (counter monotone within the launch).  The
-// payload crosses in the guide's valid form (MI355X_MICROARCH.md "Valid forms", row 1): sc1 stores
-// and loads, each storing wave's s_waitcnt vmcnt(0) before the barrier, relaxed agent counter.
-__device__ __forceinline__ void grid_sync(int* cnt, int target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
-  }
-  __syncthreads();
-}
-
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ptr_rsrc(const void* p, size_t bytes) {
   const uint64_t a = (uint64_t)p;
@@ -84,20 +71,27 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int e, double v
 
 // Householder QR of the m x kB panel P (column-major, ld lda) in place, LAPACK dgeqr2's layout
 // (R on and above the diagonal, v below it with v_0 = 1 implied, tau[j]).  Thread = row; the
-// workgroups are co-resident (gridDim.x <= CUs), one grid barrier per column.  part: 2 x gridDim.x
-// x (kB + 1) doubles, piv: 2 x kB doubles; cnt counts on from base (zeroed once per reduction, the
-// host adds each panel's kB x gridDim.x arrivals to base).
+// workgroups are co-resident (gridDim.x <= CUs).  Column j's partial sums (part[(j G + g)(kB + 1)
+// + k]) and pivot row (piv[j kB + k]) are written once each (sc1) into slots that hold the
+// all-ones sentinel before the launch; every workgroup polls the values themselves (a slot still
+// holding the sentinel is read again), so a column costs one store-to-load round trip and no
+// barrier (the mailbox form of the chase; the polls give up after ~2^22 rounds, never hanging on a
+// NaN input).
+constexpr unsigned long long kSentinel = ~0ull;
+__device__ __forceinline__ bool is_sentinel(double v) {
+  return __builtin_bit_cast(unsigned long long, v) == kSentinel;
+}
 __global__ void __launch_bounds__(kPanelRows)
 k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
-           double* __restrict__ piv, int* __restrict__ cnt, int base) {
+           double* __restrict__ piv) {
   __shared__ double red[kPanelRows / 64][kB];
   __shared__ double red8[8][kB];
   __shared__ double tot[kB];
   __shared__ double prow[kB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = gridDim.x;
-  const __amdgpu_buffer_rsrc_t prs = ptr_rsrc(part, (size_t)2 * G * (kB + 1) * 8);
-  const __amdgpu_buffer_rsrc_t vrs = ptr_rsrc(piv, (size_t)2 * kB * 8);
+  const __amdgpu_buffer_rsrc_t prs = ptr_rsrc(part, (size_t)kB * G * (kB + 1) * 8);
+  const __amdgpu_buffer_rsrc_t vrs = ptr_rsrc(piv, (size_t)kB * kB * 8);
   const int r = blockIdx.x * kPanelRows + tid;
   const bool own = r < m;
   double x[kB];
@@ -105,8 +99,7 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
   for (int k = 0; k < kB; ++k) x[k] = own ? P[(size_t)k * lda + r] : 0.0;
   const int kmax = min(m, kB);
   for (int j = 0; j < kmax; ++j) {
-    const int par = j & 1;
-    const int pj = (par * G + blockIdx.x) * (kB + 1);
+    const int pj = (j * G + blockIdx.x) * (kB + 1);
     // slot j: sum of squares of x_j below row j; slot k > j: sum of x_j x_k below row j
     const bool below = own && r > j;
     double xj = 0.0;
@@ -121,24 +114,35 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
     }
     if (own && r == j) {
 #pragma unroll
-      for (int k = 0; k < kB; ++k) bstore(vrs, par * kB + k, x[k]);
+      for (int k = 0; k < kB; ++k)
+        if (k >= j) bstore(vrs, j * kB + k, x[k]);
     }
     __syncthreads();
     if (tid < kB && tid >= j) bstore(prs, pj + tid, red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
-    grid_sync(cnt, base + (j + 1) * G);
     {  // the G partials: thread (k, g0) sums g = g0, g0 + 8, ... (G <= 128), then the 8 in fixed order
       const int k = tid & 31, g0 = tid >> 5;
       double pv[16];
+      auto slot = [&](int q) { return (j * G + g0 + 8 * q) * (kB + 1) + k; };
+      auto live = [&](int q) { return k >= j && g0 + 8 * q < G; };
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int g = g0 + 8 * q;
-        pv[q] = (k >= j && g < G) ? bload(prs, (par * G + g) * (kB + 1) + k) : 0.0;
+      for (int q = 0; q < 16; ++q) pv[q] = live(q) ? bload(prs, slot(q)) : 0.0;
+      double pr = tid < kB && tid >= j ? bload(vrs, j * kB + tid) : 0.0;
+      for (int it = 0; it < (1 << 22); ++it) {
+        bool miss = is_sentinel(pr);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) miss |= is_sentinel(pv[q]);
+        if (!miss) break;
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          if (is_sentinel(pv[q])) pv[q] = bload(prs, slot(q));
+        if (is_sentinel(pr)) pr = bload(vrs, j * kB + tid);
       }
       double s = 0.0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) s += pv[q];
       red8[g0][k] = s;
-      if (tid < kB) prow[tid] = tid >= j ? bload(vrs, par * kB + tid) : 0.0;
+      if (tid < kB) prow[tid] = pr;
     }
     __syncthreads();
     if (tid < kB) {
@@ -794,9 +798,11 @@ k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long 
       // R(b-1, b-1) from task (s - 1, t + 2)
       if (s > 0 && mr == kB) {
         unsigned long long bits;
-        while ((bits = __hip_atomic_load(mb + (size_t)(s - 1) * MT + t + 2, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)) == ~0ull)
+        for (int it = 0; it < (1 << 24); ++it) {  // bounded: never hangs on a NaN (sentinel) value
+          bits = __hip_atomic_load(mb + (size_t)(s - 1) * MT + t + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (bits != ~0ull) break;
           __builtin_amdgcn_s_sleep(1);
+        }
         if (j == kB - 1 && h == 1) Rm[15] = __builtin_bit_cast(double, bits);
       }
       wave_sync();
@@ -1244,7 +1250,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.Yp = (double*)take((size_t)((n / kT + 1 + kSymmCh - 1) / kSymmCh) * kB * n * 8);
   w.M = (double*)take((size_t)kB * kB * 8);
   w.Gm = (double*)take((size_t)kB * kB * 8);
-  w.part = (double*)take((size_t)2 * 128 * (kB + 1) * 8);
+  w.part = (double*)take(((size_t)kB * 128 * (kB + 1) + (size_t)kB * kB) * 8);  // + the pivot rows
   w.piv = (double*)take((size_t)2 * kB * 8);
   w.part2 = (double*)take(((size_t)n / 256 + 2) * kB * kB * 8);
   w.S = (double*)take((size_t)n * kLD * 8);
@@ -1284,16 +1290,15 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
       hipEventCreateWithFlags(&evS, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&evP, hipEventDisableTiming) != hipSuccess)
     return -1;
-  int cbase = 0;
   // the panel at column i: QR, V copies, V^T V partials, T, on stream q
   auto factor = [&](int i, int p, hipStream_t q) -> int {
     const int m = n - i - kB, par = p & 1;
     double* P = A + (size_t)i * lda + i + kB;
     const int G = (m + kPanelRows - 1) / kPanelRows, ng = (m + 255) / 256, k = std::min(m, kB);
     if (G > 128) return -2;
-    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, q, P, lda, m, ws.tau1 + i, ws.part, ws.piv, ws.cnt,
-                       cbase);
-    cbase += kB * G;
+    if (hipMemsetAsync(ws.part, 0xff, ((size_t)kB * G * (kB + 1) + (size_t)kB * kB) * 8, q) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, q, P, lda, m, ws.tau1 + i, ws.part,
+                       ws.part + (size_t)kB * G * (kB + 1));
     hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256), dim3(256), 0, q, P, lda, m, k, ws.Vw2[par], ws.Vt2[par]);
     hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, q, ws.Vw2[par], ws.Vw2[par], m, ws.part2v);
     hipLaunchKernelGGL(k_sb_tmat, dim3(1), dim3(kB * kB), 0, q, ws.part2v, ng, k, ws.tau1 + i,
