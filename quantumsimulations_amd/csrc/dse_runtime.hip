@@ -1840,8 +1840,8 @@ bool dense_eligible(const HostProblem& P) {
 // profiles/r03/ab/sytrd_column_kernels_ab.jsonl)
 constexpr size_t kEigHalfMinDim = 2048;
 // eig_impl 1 from 2^14: eig_sym_2stage (dse_eig2.hip: band reduction, bulge chase, dstedc, Q2, Q1)
-// measured 1.79 s against eig_sym_lower's 2.35 s at 2^14 (profiles/r04/eig2_probe.jsonl); at 2^12
-// 0.19 s against 0.13 s
+// measured 1.43 s against eig_sym_lower's 2.25 s at 2^14, 0.428 against 0.430 s at 2^13
+// (profiles/r04/eig_one_vs_two_stage.jsonl)
 constexpr size_t kEig2MinDim = 16384;
 
 // Seconds of device time, by the measured rates: the Chebyshev propagator at ~15 TF/s of its
@@ -1862,7 +1862,7 @@ bool dense_cheaper(const HostProblem& P, const double* t, int n_t, bool half_eig
   double eig = half_eig && dim >= (double)kEigHalfMinDim
                    ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
                    : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
-  if (half_eig && dim >= (double)kEig2MinDim) eig *= 0.66;  // two-stage: 1.55 vs 2.35 s at 2^14
+  if (half_eig && dim >= (double)kEig2MinDim) eig *= 0.61;  // two-stage: 1.43 vs 2.35 s at 2^14
   const double dense = eig + 4.0 * dim * dim * n_t / 40e12 + (double)n_t * dim * P.n_local * 32.0 / 2e12;
   return dense < cheb;
 }

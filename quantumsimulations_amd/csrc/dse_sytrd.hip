@@ -390,13 +390,18 @@ k_trd_wfix(const double* __restrict__ A, int lda, TrdWs ws, int ldw, int n, int 
 }
 
 // ---- back-transformation V = Q Z, Q = H(0) H(1) ... H(n-2) (LAPACK dormtr, left, lower) ----
-// Blocks of kOrmKB reflectors from the last to the first, each applied as I - Vb T Vb^T in the
+// Blocks of orm_kb(n) reflectors from the last to the first, each applied as I - Vb T Vb^T in the
 // "UT" form T = S^{-1}, S = diag(1 / tau) + striu(Vb^T Vb): Wt = Vb^T Z_b (GEMM), Wt = S^{-1} Wt
-// (TRSM), Z_b -= Vb Wt (GEMM), where Z_b = the rows i+1 .. n-1 the block acts on.  A block of 256
+// (TRSM), Z_b -= Vb Wt (GEMM), where Z_b = the rows i+1 .. n-1 the block acts on.  A block of k
 // reflectors reads Z_b three times (rocSOLVER dormtr's blocks of 32: ~24 passes over the same
 // rows; measured 769 ms at 2^14, 11 TF/s).  A reflector with tau = 0 (H = I: its column was zero
-// already) gets a zero column in Vb and 1 on S's diagonal, so it changes nothing.
-constexpr int kOrmKB = 256;
+// already) gets a zero column in Vb and 1 on S's diagonal, so it changes nothing.  Block size
+// (round 4, probe_eig2's Q1 at 2^14 / 2^13, profiles/r04/orm_block_ab.txt): 256 -> 235 / -, 512 ->
+// 204, 1024 -> 169 / 24, 2048 -> 160 / 28, 4096 -> 190 / 38 ms.
+#ifndef DSE_ORM_KB
+#define DSE_ORM_KB 0
+#endif
+inline int orm_kb(int n) { return DSE_ORM_KB > 0 ? DSE_ORM_KB : n >= 16384 ? 2048 : 1024; }
 constexpr int kHalfTrdMinDim = 8192;
 
 // Vb (m_b x k, column-major): unit lower trapezoid of the reflectors i .. i+k-1 (reflector q of
@@ -438,7 +443,8 @@ TrdWs carve(double* work, int n) {
 size_t sytrd_workspace(int n) {
   const size_t nbk = ((size_t)n + kTrdBS - 1) / kTrdBS, ng = ((size_t)n + kTrdRows - 1) / kTrdRows;
   const size_t trd = (size_t)n * kTrdNB + nbk * nbk * kTrdBS + ng * 2 * kTrdNB + 2 * kTrdNB + nbk + kTrdNB + ng + 2;
-  const size_t orm = 2 * (size_t)n * kOrmKB + (size_t)kOrmKB * kOrmKB;  // Vb, Wt, S
+  const size_t kb = (size_t)orm_kb(n);
+  const size_t orm = 2 * (size_t)n * kb + kb * kb;  // Vb, Wt, S
   return std::max(trd, orm) * sizeof(double);
 }
 
@@ -446,6 +452,7 @@ int ormtr_lower(rocblas_handle h, hipStream_t st, int n, const double* A, int ld
                 int ldz, double* work, int off) {
   const int nref = n - off;
   if (nref <= 0) return 0;
+  const int kOrmKB = orm_kb(n);
   double* Vb = work;
   double* Wt = Vb + (size_t)n * kOrmKB;
   double* S = Wt + (size_t)n * kOrmKB;
