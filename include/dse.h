@@ -179,7 +179,7 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "eig_impl"     dense engine eigensolver: 0 rocSOLVER dsyevd; 1 (default) for
  *                         registers of >= 2^11 amplitudes a tridiagonalisation (the half-matrix
  *                         one of dse_sytrd.hip from 2^13, rocSOLVER's below), rocSOLVER dstedc
- *                         and a blocked back-transformation, dsyevd below 2^11, and from 2^14
+ *                         and a blocked back-transformation, dsyevd below 2^11, and from 2^13
  *                         the two-stage solver of dse_eig2.hip (dense -> band 32 -> tridiagonal
  *                         by bulge chasing, dstedc, both back-transformations); 2 the half-matrix
  *                         path from 2^10; 3 the two-stage solver from 2^10.  Costs one extra

@@ -239,7 +239,7 @@ k_sb_tmat(const double* __restrict__ part, int ng, int k, const double* __restri
 // cdna_hip_programming.md) ----
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int kT = 64;       // tile of the trailing matrix
-constexpr int kTP = kT + 4;  // LDS row pitch (doubles): 8 r + 2 k distinct banks over a 16-lane group
+
 
 __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);

@@ -1839,10 +1839,14 @@ bool dense_eligible(const HostProblem& P) {
 // 0.46 vs 0.68 s at 2^13, 2.35 vs 4.12 s at 2^14 (profiles/r03/sytrd_probe.jsonl,
 // profiles/r03/ab/sytrd_column_kernels_ab.jsonl)
 constexpr size_t kEigHalfMinDim = 2048;
-// eig_impl 1 from 2^14: eig_sym_2stage (dse_eig2.hip: band reduction, bulge chase, dstedc, Q2, Q1)
+// eig_impl 1 from 2^13: eig_sym_2stage (dse_eig2.hip: band reduction, bulge chase, dstedc, Q2, Q1)
 // measured 1.43 s against eig_sym_lower's 2.25 s at 2^14, 0.428 against 0.430 s at 2^13
-// (profiles/r04/eig_one_vs_two_stage.jsonl)
-constexpr size_t kEig2MinDim = 16384;
+// (profiles/r04/eig_one_vs_two_stage.jsonl); an N = 14 point of the 30 s grid (two 2^14 registers,
+// one 2^13, three solver streams) 3.46-3.75 s with the 2^13 one two-stage against 3.62-3.72 s
+// one-stage (profiles/r04/eig_impl_point_ab.jsonl).  Per-register output GEMMs (a register's outputs
+// as soon as it is solved, instead of a job's) measured 3.66-3.77 s against 3.45-3.62 s and were
+// dropped (profiles/r04/eig_point_outputs_per_register.jsonl).
+constexpr size_t kEig2MinDim = 8192;
 
 // Seconds of device time, by the measured rates: the Chebyshev propagator at ~15 TF/s of its
 // algorithmic FP64 work (the N = 14 bench runs at 16.5 chip-level) with ~25 extra terms per
@@ -1862,7 +1866,7 @@ bool dense_cheaper(const HostProblem& P, const double* t, int n_t, bool half_eig
   double eig = half_eig && dim >= (double)kEigHalfMinDim
                    ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
                    : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
-  if (half_eig && dim >= (double)kEig2MinDim) eig *= 0.61;  // two-stage: 1.43 vs 2.35 s at 2^14
+  if (half_eig && dim >= 16384.0) eig *= 0.61;  // two-stage: 1.43 vs 2.35 s at 2^14
   const double dense = eig + 4.0 * dim * dim * n_t / 40e12 + (double)n_t * dim * P.n_local * 32.0 / 2e12;
   return dense < cheb;
 }

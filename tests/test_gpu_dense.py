@@ -16,8 +16,8 @@ output time exact from one GEMM (rocBLAS dgemm) and the observable pass.
 * the half-matrix eigensolver (csrc/dse_sytrd.hip, option eig_impl): config 2 through it at dim 4096
   against the exact fixture (1e-10) and against rocSOLVER dsyevd (1e-11); an N = 13 register (dim
   8192, its default range) against dsyevd on a 1 s grid, to the phase drift of eigenvalue rounding
-* the two-stage eigensolver (csrc/dse_eig2.hip, eig_impl 3; eig_impl 1 takes it from 2^14, so the
-  N = 14 tests above run it): config 2 at dim 4096 against the exact fixture and dsyevd, and an
+* the two-stage eigensolver (csrc/dse_eig2.hip, eig_impl 3; eig_impl 1 takes it from 2^13, so the
+  N = 14 tests above run it; the half-matrix one keeps its N = 13 test through eig_impl 2): config 2 at dim 4096 against the exact fixture and dsyevd, and an
   N = 13 register against dsyevd as for the half-matrix one
 """
 import json
@@ -185,7 +185,7 @@ def test_half_eigensolver_config2_matches_exact_and_dsyevd(engine, golden):
 def test_half_eigensolver_n13_matches_dsyevd(engine):
     t = np.linspace(0.0, 1.0, 2001)
     p = sweep_point_params(12, 100e3, "center_on", 1.0, 2001)
-    hm, st, s_hm = _evolve(engine, [p], t, 2, eig_impl=1)
+    hm, st, s_hm = _evolve(engine, [p], t, 2, eig_impl=2)
     ev, _, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
     assert st["dense_problems"] == 1
     np.testing.assert_allclose(hm[:, 6], 1.0, atol=1e-10)
