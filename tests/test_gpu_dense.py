@@ -220,3 +220,18 @@ def test_two_stage_eigensolver_n13_matches_dsyevd(engine):
     tol = 1e-11 + 1e-8 * t  # as for the half-matrix solver: eigenvalue rounding drift
     assert np.all(np.abs(ts - ev) <= tol), np.max(np.abs(ts - ev) - tol)
     assert np.max(np.abs(s_ts[0] - s_ev[0])) < 1e-8
+
+
+@pytest.mark.parametrize("n_sea", [9, 10])
+def test_two_stage_eigensolver_small_registers_match_dsyevd(engine, n_sea):
+    """2^10 / 2^11 registers (eig_impl 3 takes them; edge tiles of the band reduction, short sweeps
+    of the chase) against dsyevd on a 0.2 s grid."""
+    t = np.linspace(0.0, 0.2, 401)
+    p = sweep_point_params(n_sea, 40e3, "shell_off", 0.2, 401)
+    ts, st, s_ts = _evolve(engine, [p], t, 2, eig_impl=3)
+    ev, _, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st["dense_problems"] == 1
+    np.testing.assert_allclose(ts[:, 6], 1.0, atol=1e-10)
+    tol = 1e-11 + 1e-8 * t
+    assert np.all(np.abs(ts - ev) <= tol), np.max(np.abs(ts - ev) - tol)
+    assert np.max(np.abs(s_ts[0] - s_ev[0])) < 1e-8
