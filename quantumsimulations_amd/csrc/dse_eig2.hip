@@ -929,10 +929,12 @@ constexpr int kQ2Waves = 4;
 // DMA: the group records go global -> LDS directly (global_load_lds, 16 B per lane, double-buffered,
 // no staging registers); W waves per workgroup.
 constexpr int kQ2Dma = (kQ2Rec * 8 + 1023) / 1024;  // 1-KiB copies per group
-template <int NC, bool PF, bool PAIR, bool DMA, int W>
+// SC: the reflector values are read with scalar loads straight from the records (uniform across the
+// wave: SGPR operands of the FMAs, no LDS traffic); the records are written by earlier launches.
+template <int NC, bool PF, bool PAIR, bool DMA, int W, bool SC = false>
 __global__ void __launch_bounds__(64 * W)
 k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl, const long long* __restrict__ goff) {
-  constexpr int kBuf = DMA ? 2 * kQ2Dma * 128 : kQ2PerLane * 64;  // doubles per wave
+  constexpr int kBuf = SC ? 2 : DMA ? 2 * kQ2Dma * 128 : kQ2PerLane * 64;  // doubles per wave
   __shared__ __attribute__((aligned(16))) double rvs[W][kBuf];
   __shared__ int state[W];  // (block order index) * 65536 + groups done (65535: block done)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -977,7 +979,8 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
       for (int q = 0; q < kQ2Dma; ++q)
         __builtin_amdgcn_global_load_lds(src + q * 1024, (__attribute__((address_space(3))) void*)(dst + q * 128), 16, 0, 0);
     };
-    if constexpr (DMA) {
+    if constexpr (SC) {
+    } else if constexpr (DMA) {
       dma(0);
     } else {
 #pragma unroll
@@ -1005,7 +1008,12 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
         }
       }
       const double* rg = rv;  // this group's records
-      if constexpr (DMA) {
+      if constexpr (SC) {
+        const uint64_t ga = (uint64_t)(gb + (size_t)t * kQ2Rec);
+        const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ga >> 32));
+        const uint32_t glo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ga);  // unsigned: no sign extension
+        rg = (const double*)(((uint64_t)ghi << 32) | (uint64_t)glo);
+      } else if constexpr (DMA) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // group t's copy (and the window rows) landed
         __builtin_amdgcn_wave_barrier();
         rg = rv + (t & 1) * kQ2Dma * 128;
@@ -1027,8 +1035,11 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
       if constexpr (!PAIR) {  // one reflector at a time
 #pragma unroll
         for (int u = kQ2NB - 1; u >= 0; --u) {
-          const double* r = rg + u * kRec;
-          const double tau = r[kB];
+          typedef const __attribute__((address_space(4))) double* kptr;
+          const kptr r = SC ? (kptr)(rg + u * kRec) : (kptr) nullptr;
+          const double* rl = rg + u * kRec;
+          auto rval = [&](int k) -> double { return SC ? r[k] : rl[k]; };
+          const double tau = rval(kB);
           if (tau == 0.0) continue;  // uniform
           double d[NC][4];
 #pragma unroll
@@ -1039,7 +1050,7 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
           for (int k = 0; k < kB; k += 4)
 #pragma unroll
             for (int x = 0; x < 4; ++x) {
-              const double p = r[k + x];
+              const double p = rval(k + x);
 #pragma unroll
               for (int c = 0; c < NC; ++c) d[c][x] = fma(p, win[c][u + k + x], d[c][x]);
             }
@@ -1048,7 +1059,7 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
           for (int c = 0; c < NC; ++c) g[c] = tau * ((d[c][0] + d[c][1]) + (d[c][2] + d[c][3]));
 #pragma unroll
           for (int k = 0; k < kB; ++k) {
-            const double p = r[k];
+            const double p = rval(k);
 #pragma unroll
             for (int c = 0; c < NC; ++c) win[c][u + k] = fma(-g[c], p, win[c][u + k]);
           }
@@ -1183,7 +1194,8 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
 // k_sb_q2 variant (set_eig2_q2_variant; 2^14, profiles/r04/eig2_q2_variants.txt): 0 one
 // reflector at a time, rows loaded after each group (346 ms); 1 pairs + the next rows under the
 // group (361); 2 two columns per lane (649); 3 pairs (357); 4 = 0 with the records copied global ->
-// LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default)
+// LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default); 6 / 7 the reflector values
+// as scalar-load SGPR operands, 8 / 4 waves (512 / 921: each reflector waits on its s_loads)
 int g_q2_variant = 5;
 // the chase: 0 k_sb2st (waits for (s - 1, t + 2) complete), 1 k_sb2st_pf (default)
 int g_chase_variant = 1;
@@ -1380,6 +1392,8 @@ int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
     case 3: hipLaunchKernelGGL((k_sb_q2<1, false, true, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 4: hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 5: hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 8>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 6: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 8, true>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 7: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4, true>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     default: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
   }
   // back: Z(r, c) = Zt[r n + c], i.e. the column-major read of Zt^T
