@@ -106,11 +106,23 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
 #pragma unroll
     for (int k = 0; k < kB; ++k) xj = k == j ? x[k] : xj;
     if (!below) xj = 0.0;
+    {  // the wave's 32 sums x_j . x_k by a butterfly reduce-scatter (31 exchanges instead of 32 x 6):
+       // after the steps over lane bits 5 .. 1 lane l holds k = l >> 1 over its half, bit 0 adds the pair
+      double pk[kB];
 #pragma unroll
-    for (int k = 0; k < kB; ++k) {
-      if (k < j) continue;
-      const double s = wave_sum(xj * x[k]);
-      if (lane == 0) red[wave][k] = s;
+      for (int k = 0; k < kB; ++k) pk[k] = xj * x[k];
+#pragma unroll
+      for (int o = 32, h = 16; o >= 2; o >>= 1, h >>= 1) {
+        const bool up = (lane & o) != 0;
+#pragma unroll
+        for (int q = 0; q < h; ++q) {
+          const double send = up ? pk[q] : pk[q + h];
+          const double keep = up ? pk[q + h] : pk[q];
+          pk[q] = keep + __shfl_xor(send, o, 64);
+        }
+      }
+      const double sk = pk[0] + __shfl_xor(pk[0], 1, 64);
+      if ((lane & 1) == 0) red[wave][lane >> 1] = sk;
     }
     if (own && r == j) {
 #pragma unroll
