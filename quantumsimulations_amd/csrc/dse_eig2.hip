@@ -757,6 +757,9 @@ k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long lon
 // mailbox mb[(s - 1) MT + t + 2] as soon as it has it and never stores the element; the consumer
 // polls the mailbox (8-B sc1, sentinel all-ones) instead of waiting for the whole task.  So task
 // (s, t) waits for (s - 1, t + 1) complete + beta of (s - 1, t + 2) (was: (s - 1, t + 2) complete).
+// EARLY: the next task's D / R loads are issued before this task's stores (their blocks are
+// disjoint), so the store drain before the progress flag also lands them.
+template <bool EARLY>
 __global__ void __launch_bounds__(64 * kChaseWG)
 k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long long* __restrict__ goff,
            int* __restrict__ prog, unsigned long long* __restrict__ mb, int MT) {
@@ -881,6 +884,12 @@ k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long 
           for (int q = 0; q < 16; ++q) Rm[q] = fma(-z, vh[q], Rm[q]);
         }
       }
+      if (EARLY && t + 1 < nt) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Lcar[q] = Rm[q];
+        wait_prog(min(ntp, t + 3));
+        load_dr(t + 1);
+      }
       // stores: L always (a carried L is only in registers), but L(0, 0) from t = 2 on (the
       // consumer's); D when changed; R stays in registers (the next task's L)
       wave_sync();  // every lane's reads of Lt / Dt above are done
@@ -901,7 +910,7 @@ k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long 
       if (lane < kB) rf[lane] = B.v[lane];
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(prog + s, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1 < nt) {
+      if (!EARLY && t + 1 < nt) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) Lcar[q] = Rm[q];
         wait_prog(min(ntp, t + 3));
@@ -1209,7 +1218,9 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
 // LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default); 6 / 7 the reflector values
 // as scalar-load SGPR operands, 8 / 4 waves (512 / 921: each reflector waits on its s_loads)
 int g_q2_variant = 5;
-// the chase: 0 k_sb2st (waits for (s - 1, t + 2) complete), 1 k_sb2st_pf (default)
+// the chase: 0 k_sb2st (waits for (s - 1, t + 2) complete: 336 ms at 2^14), 1 k_sb2st_pf (243 ms,
+// default), 2 k_sb2st_pf with the next task's loads issued before the stores (280 ms: the progress
+// flag then waits for sweep s - 1 too)
 int g_chase_variant = 1;
 
 struct Eig2Ws {
@@ -1384,7 +1395,10 @@ int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, doub
   else {
     const int MT = chase_tasks(n, 0) + 1;
     if (hipMemsetAsync(ws.mb, 0xff, (size_t)n * MT * 8, st) != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_sb2st_pf, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb, MT);
+    if (g_chase_variant == 2)
+      hipLaunchKernelGGL(k_sb2st_pf<true>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb, MT);
+    else
+      hipLaunchKernelGGL(k_sb2st_pf<false>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb, MT);
   }
   hipLaunchKernelGGL(k_sb_tridiag, dim3((n + 255) / 256), dim3(256), 0, st, ws.S, n, d, e);
   if (hipStreamSynchronize(st) != hipSuccess) return -1;  // goff is host memory until here
