@@ -83,7 +83,7 @@ __device__ __forceinline__ bool is_sentinel(double v) {
 }
 __global__ void __launch_bounds__(kPanelRows)
 k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
-           double* __restrict__ piv) {
+           double* __restrict__ piv, double* __restrict__ Vw, double* __restrict__ Vt) {
   __shared__ double red[kPanelRows / 64][kB];
   __shared__ double red8[8][kB];
   __shared__ double tot[kB];
@@ -200,22 +200,15 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
     }
   }
   if (own) {
+    // the panel in place, and Vw (m x kB, ld m) / Vt (row-major) of the reflectors with their unit
+    // diagonal, zeros above it and past kmax (written here from the registers)
 #pragma unroll
-    for (int k = 0; k < kB; ++k) P[(size_t)k * lda + r] = x[k];
-  }
-}
-
-// Vw (m x kB, ld m) and its row-major copy Vt (Vt[r kB + q]): the panel's reflectors with their
-// unit diagonal, zeros above it and past k
-__global__ void __launch_bounds__(256)
-k_sb_vcopy(const double* __restrict__ P, int lda, int m, int k, double* __restrict__ Vw, double* __restrict__ Vt) {
-  const int r = (int)(blockIdx.x * 256 + threadIdx.x);
-  if (r >= m) return;
-#pragma unroll 4
-  for (int q = 0; q < kB; ++q) {
-    const double v = q >= k ? 0.0 : r > q ? P[(size_t)q * lda + r] : (r == q ? 1.0 : 0.0);
-    Vw[(size_t)q * m + r] = v;
-    Vt[(size_t)r * kB + q] = v;
+    for (int k = 0; k < kB; ++k) {
+      P[(size_t)k * lda + r] = x[k];
+      const double v = k >= kmax ? 0.0 : r > k ? x[k] : (r == k ? 1.0 : 0.0);
+      Vw[(size_t)k * m + r] = v;
+      Vt[(size_t)r * kB + k] = v;
+    }
   }
 }
 
@@ -1333,8 +1326,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     if (G > 128) return -2;
     if (hipMemsetAsync(ws.part, 0xff, ((size_t)kB * G * (kB + 1) + (size_t)kB * kB) * 8, q) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, q, P, lda, m, ws.tau1 + i, ws.part,
-                       ws.part + (size_t)kB * G * (kB + 1));
-    hipLaunchKernelGGL(k_sb_vcopy, dim3((m + 255) / 256), dim3(256), 0, q, P, lda, m, k, ws.Vw2[par], ws.Vt2[par]);
+                       ws.part + (size_t)kB * G * (kB + 1), ws.Vw2[par], ws.Vt2[par]);
     hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, q, ws.Vw2[par], ws.Vw2[par], m, ws.part2v);
     hipLaunchKernelGGL(k_sb_tmat, dim3(1), dim3(kB * kB), 0, q, ws.part2v, ng, k, ws.tau1 + i,
                        ws.T + (size_t)p * kB * kB);
