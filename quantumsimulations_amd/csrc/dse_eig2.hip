@@ -493,27 +493,33 @@ k_sb_gm(const double* __restrict__ part, int ng, int k, const double* __restrict
   Gm[(size_t)q * kB + p] = (p < k && q < k) ? gsum : 0.0;
 }
 
-// W = Y2 - V Gm / 2 row-wise in place (into Y)
+// Wt (row-major m x kB) = Y2 - V Gm / 2; 64 rows per workgroup: thread (r, 8 of the 32 q) from the
+// column-major V and Y (coalesced along r), the 64 x 32 result through LDS to whole Wt rows
 __global__ void __launch_bounds__(256)
-k_sb_w(double* __restrict__ Y, const double* __restrict__ V, int m, int k, const double* __restrict__ Gm,
+k_sb_w(const double* __restrict__ Y, const double* __restrict__ V, int m, int k, const double* __restrict__ Gm,
        double* __restrict__ Wt) {
   __shared__ double Gs[kB][kB];
-  const int tid = threadIdx.x, r = blockIdx.x * 256 + tid;
+  __shared__ double Ws[64][kB + 1];
+  const int tid = threadIdx.x, rl = tid & 63, qg = tid >> 6, r0 = blockIdx.x * 64, r = r0 + rl;
   for (int e = tid; e < kB * kB; e += 256) Gs[e % kB][e / kB] = Gm[e];
   __syncthreads();
-  if (r >= m) return;
-  double v[kB];
+  if (r < m) {
+    double v[kB];
 #pragma unroll
-  for (int p = 0; p < kB; ++p) v[p] = p < k ? V[(size_t)p * m + r] : 0.0;
+    for (int p = 0; p < kB; ++p) v[p] = p < k ? V[(size_t)p * m + r] : 0.0;
 #pragma unroll
-  for (int q = 0; q < kB; ++q) {
-    if (q >= k) continue;
-    double a = 0.0;
+    for (int qq = 0; qq < 8; ++qq) {
+      const int q = 8 * qg + qq;
+      double a = 0.0;
 #pragma unroll
-    for (int p = 0; p < kB; ++p) a = fma(v[p], Gs[p][q], a);
-    const double wv = Y[(size_t)q * m + r] - 0.5 * a;
-    Y[(size_t)q * m + r] = wv;
-    Wt[(size_t)r * kB + q] = wv;
+      for (int p = 0; p < kB; ++p) a = fma(v[p], Gs[p][q], a);
+      Ws[rl][q] = q < k ? Y[(size_t)q * m + r] - 0.5 * a : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < 64 * kB; e += 256) {
+    const int rr = e >> 5, q = e & 31;
+    if (r0 + rr < m) Wt[(size_t)(r0 + rr) * kB + q] = Ws[rr][q];
   }
 }
 
@@ -1350,7 +1356,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     hipLaunchKernelGGL(k_sb_yt2, dim3((m + 7) / 8), dim3(256), 0, st, ws.Y, ws.Yp, m, k, T);
     hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, st, Vw, ws.Yp, m, ws.part2);
     hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
-    hipLaunchKernelGGL(k_sb_w, dim3(ng), dim3(256), 0, st, ws.Yp, Vw, m, k, ws.Gm, ws.Wt);
+    hipLaunchKernelGGL(k_sb_w, dim3((m + 63) / 64), dim3(256), 0, st, ws.Yp, Vw, m, k, ws.Gm, ws.Wt);
     if (i + kB < last) {
       hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, 1), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, kB);
       if (hipEventRecord(evS, st) != hipSuccess || hipStreamWaitEvent(s2, evS, 0) != hipSuccess) rc = -1;
