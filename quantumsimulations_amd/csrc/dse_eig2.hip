@@ -431,18 +431,19 @@ k_sb_ysum(double* __restrict__ Y, const double* __restrict__ Yp, int nch, int m)
   Y[e] = a;
 }
 
-// part[g] (kB x kB, column-major) = V_g^T Y_g over the 256-row chunk g, on the matrix cores
-// (4 waves: wave w takes the chunk's rows 64 w .. 64 w + 63, the four 16 x 16 output tiles; the
-// waves' sums are added in fixed order)
+// part[g] (kB x kB, column-major) = V_g^T Y_g over the kVtyRows-row chunk g, on the matrix cores
+// (4 waves: wave w takes a quarter of the chunk's rows, the four 16 x 16 output tiles; the waves'
+// sums are added in fixed order).  128-row chunks: 74 KB of LDS, two workgroups per CU.
+constexpr int kVtyRows = 128;
 __global__ void __launch_bounds__(256)
 k_sb_vty(const double* __restrict__ V, const double* __restrict__ Y, int m, double* __restrict__ part) {
-  __shared__ double Vs[256][kB + 4];
-  __shared__ double Ys[256][kB + 4];
+  __shared__ double Vs[kVtyRows][kB + 4];
+  __shared__ double Ys[kVtyRows][kB + 4];
   double(*red)[kB * kB] = reinterpret_cast<double(*)[kB * kB]>(&Vs[0][0]);  // after the products
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rb = blockIdx.x * 256;
-  for (int e = tid; e < 256 * kB; e += 256) {
-    const int r = e & 255, q = e >> 8;
+  const int rb = blockIdx.x * kVtyRows;
+  for (int e = tid; e < kVtyRows * kB; e += 256) {
+    const int r = e % kVtyRows, q = e / kVtyRows;
     const bool ok = rb + r < m;
     Vs[r][q] = ok ? V[(size_t)q * m + rb + r] : 0.0;
     Ys[r][q] = ok ? Y[(size_t)q * m + rb + r] : 0.0;
@@ -455,8 +456,8 @@ k_sb_vty(const double* __restrict__ V, const double* __restrict__ Y, int m, doub
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
-    const int r = 64 * w + 4 * kk + (lane >> 4);
+  for (int kk = 0; kk < kVtyRows / 16; ++kk) {
+    const int r = (kVtyRows / 4) * w + 4 * kk + (lane >> 4);
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
       const double va = Vs[r][16 * a + (lane & 15)];
@@ -1235,7 +1236,7 @@ struct Eig2Ws {
   double* M;        // b x b
   double* Gm;       // b x b
   double* part;     // 2 x 128 x (b + 1)
-  double* part2;    // (n / 256 + 2) x b x b: V^T Y partials
+  double* part2;    // (n / kVtyRows + 2) x b x b: V^T Y partials
   double* piv;      // 2 x b
   double* S;        // n x kLD band
   double* refl;     // chase reflectors x (b + 1)
@@ -1277,7 +1278,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
     w.Vw2[q] = (double*)take((size_t)n * kB * 8);
     w.Vt2[q] = (double*)take((size_t)n * kB * 8);
   }
-  w.part2v = (double*)take(((size_t)n / 256 + 2) * kB * kB * 8);
+  w.part2v = (double*)take(((size_t)n / kVtyRows + 2) * kB * kB * 8);
   w.Y = (double*)take((size_t)n * kB * 8);
   w.Wt = (double*)take((size_t)n * kB * 8);
   w.Zt = (double*)take((size_t)n * n * 8);
@@ -1286,7 +1287,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.Gm = (double*)take((size_t)kB * kB * 8);
   w.part = (double*)take(((size_t)kB * 128 * (kB + 1) + (size_t)kB * kB) * 8);  // + the pivot rows
   w.piv = (double*)take((size_t)2 * kB * 8);
-  w.part2 = (double*)take(((size_t)n / 256 + 2) * kB * kB * 8);
+  w.part2 = (double*)take(((size_t)n / kVtyRows + 2) * kB * kB * 8);
   w.S = (double*)take((size_t)n * kLD * 8);
   w.refl = (double*)take(chase_refl_doubles(n) * 8);
   w.orm = (double*)take(sytrd_workspace(n));
@@ -1328,7 +1329,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
   auto factor = [&](int i, int p, hipStream_t q) -> int {
     const int m = n - i - kB, par = p & 1;
     double* P = A + (size_t)i * lda + i + kB;
-    const int G = (m + kPanelRows - 1) / kPanelRows, ng = (m + 255) / 256, k = std::min(m, kB);
+    const int G = (m + kPanelRows - 1) / kPanelRows, ng = (m + kVtyRows - 1) / kVtyRows, k = std::min(m, kB);
     if (G > 128) return -2;
     if (hipMemsetAsync(ws.part, 0xff, ((size_t)kB * G * (kB + 1) + (size_t)kB * kB) * 8, q) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, q, P, lda, m, ws.tau1 + i, ws.part,
@@ -1347,7 +1348,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     const double* T = ws.T + (size_t)p * kB * kB;
     const double* Vw = ws.Vw2[par];
     const double* Vt = ws.Vt2[par];
-    const int nbk = (m + kT - 1) / kT, ng = (m + 255) / 256, nch = (nbk + kSymmCh - 1) / kSymmCh;
+    const int nbk = (m + kT - 1) / kT, ng = (m + kVtyRows - 1) / kVtyRows, nch = (nbk + kSymmCh - 1) / kSymmCh;
     if (p > 0 && hipStreamWaitEvent(st, evP, 0) != hipSuccess) rc = -1;
     double* A22 = A + (size_t)(i + kB) * lda + i + kB;
     // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
