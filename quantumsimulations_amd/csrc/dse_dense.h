@@ -96,6 +96,7 @@ size_t eig2_workspace(int n);
 // Q2 application variant (probe A/B; dse_eig2.hip g_q2_variant)
 void set_eig2_q2_variant(int v);
 void set_eig2_chase_variant(int v);
+void set_eig2_syr2k_tri(int v);
 int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work);
 int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu,
                 long long* dbg = nullptr);

@@ -344,8 +344,17 @@ k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict
 // k_sb_symm); wave w takes columns c of subtile w, the A tile's loads issued first.
 __global__ void __launch_bounds__(256)
 k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, const double* __restrict__ Wt,
-           int cmin, int cmax) {
-  const int I = blockIdx.x, J = blockIdx.y;
+           int cmin, int cmax, int ntiles) {
+  // ntiles > 0: a 1-D grid over the tiles on and below the diagonal, e = I (I + 1) / 2 + J; else a
+  // 2-D grid (I, J) with the tiles above the diagonal idle
+  int I = blockIdx.x, J = blockIdx.y;
+  if (ntiles > 0) {
+    const int e = (int)blockIdx.x;
+    I = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= e) ++I;
+    while (I * (I + 1) / 2 > e) --I;
+    J = e - I * (I + 1) / 2;
+  }
   if (J > I) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lq = lane >> 4;
   const int r0 = I * kT, c0 = J * kT;
@@ -1222,6 +1231,9 @@ int g_q2_variant = 5;
 // default), 2 k_sb2st_pf with the next task's loads issued before the stores (280 ms: the progress
 // flag then waits for sweep s - 1 too)
 int g_chase_variant = 1;
+// the trailing update's grid: 0 2-D (nbk x nbk, the upper tiles idle; default), 1 1-D over the lower
+// tiles (band 413-425 vs 377 ms at 2^14: the 2-D order, I fastest, keeps a column's V/W rows warm)
+int g_syr2k_tri = 0;
 
 struct Eig2Ws {
   double* tau1;     // n: stage-1 reflectors (zero where none)
@@ -1303,6 +1315,7 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
 
 void set_eig2_q2_variant(int v) { g_q2_variant = v; }
 void set_eig2_chase_variant(int v) { g_chase_variant = v; }
+void set_eig2_syr2k_tri(int v) { g_syr2k_tri = v; }
 
 size_t eig2_workspace(int n) {
   size_t b = 0;
@@ -1349,6 +1362,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     const double* Vw = ws.Vw2[par];
     const double* Vt = ws.Vt2[par];
     const int nbk = (m + kT - 1) / kT, ng = (m + kVtyRows - 1) / kVtyRows, nch = (nbk + kSymmCh - 1) / kSymmCh;
+    const int ntri = nbk * (nbk + 1) / 2;
     if (p > 0 && hipStreamWaitEvent(st, evP, 0) != hipSuccess) rc = -1;
     double* A22 = A + (size_t)(i + kB) * lda + i + kB;
     // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
@@ -1359,13 +1373,19 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
     hipLaunchKernelGGL(k_sb_w, dim3((m + 63) / 64), dim3(256), 0, st, ws.Yp, Vw, m, k, ws.Gm, ws.Wt);
     if (i + kB < last) {
-      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, 1), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, kB);
+      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, 1), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, kB, 0);
       if (hipEventRecord(evS, st) != hipSuccess || hipStreamWaitEvent(s2, evS, 0) != hipSuccess) rc = -1;
       if (rc == 0) rc = factor(i + kB, p + 1, s2);
       if (rc == 0 && hipEventRecord(evP, s2) != hipSuccess) rc = -1;
-      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, kB, m);
+      if (g_syr2k_tri)
+        hipLaunchKernelGGL(k_sb_syr2k, dim3(ntri), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, kB, m, ntri);
+      else
+        hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, kB, m, 0);
     } else {
-      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, m);
+      if (g_syr2k_tri)
+        hipLaunchKernelGGL(k_sb_syr2k, dim3(ntri), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, m, ntri);
+      else
+        hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, m, 0);
     }
   }
   if (hipGetLastError() != hipSuccess && rc == 0) rc = -1;

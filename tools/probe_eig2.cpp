@@ -96,6 +96,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&info, sizeof(rocblas_int)));
   if (std::getenv("EIG2_Q2")) dse::set_eig2_q2_variant(std::atoi(std::getenv("EIG2_Q2")));
   if (std::getenv("EIG2_CHASE")) dse::set_eig2_chase_variant(std::atoi(std::getenv("EIG2_CHASE")));
+  if (std::getenv("EIG2_SYR2K_TRI")) dse::set_eig2_syr2k_tri(std::atoi(std::getenv("EIG2_SYR2K_TRI")));
   // EIG2_CHASE_DBG=1: the chase's per-worker phase times (k_sb2st<true>)
   long long* dbg = nullptr;
   const bool chase_dbg = std::getenv("EIG2_CHASE_DBG") && std::atoi(std::getenv("EIG2_CHASE_DBG"));
