@@ -258,7 +258,7 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 // order of the 4 k-slots works when both operands use it).  The waves' sums meet in LDS (fixed
 // order); Yp[(ch kB + q) m + r] holds chunk ch's partial.
 constexpr int kSymmCh = 16;  // column tiles per workgroup
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, double* __restrict__ Yp) {
   __shared__ double red[kB][kT + 1];
   const int I = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -271,50 +271,56 @@ k_sb_symm(const double* __restrict__ A, int lda, int m, const double* __restrict
   const int jb = ch * kSymmCh, je = min(nbk, jb + kSymmCh);
   for (int J = jb + w; J < je; J += 4) {
     const int c0 = J * kT;
-    double a[4][16], b[2][16];
     const bool full = J != I && r0 + kT <= m && c0 + kT <= m;
-    if (full && J < I) {
+    // the tile in two halves of 32 columns (registers for two workgroups per CU)
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+    for (int hf = 0; hf < 2; ++hf) {
+      double a[4][8], b[2][8];
+      if (full && J < I) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
+        for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
-          for (int rs = 0; rs < 4; ++rs)
-            a[rs][2 * u + e] = A[(size_t)(c0 + 8 * u + 2 * lq + e) * lda + r0 + 16 * rs + li];
-    } else if (full) {
+          for (int e = 0; e < 2; ++e)
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+            for (int rs = 0; rs < 4; ++rs)
+              a[rs][2 * uu + e] = A[(size_t)(c0 + 8 * (4 * hf + uu) + 2 * lq + e) * lda + r0 + 16 * rs + li];
+      } else if (full) {
 #pragma unroll
-        for (int rs = 0; rs < 4; ++rs) {
-          const double2 v = *reinterpret_cast<const double2*>(A + (size_t)(r0 + 16 * rs + li) * lda + c0 + 8 * u + 2 * lq);
-          a[rs][2 * u] = v.x;
-          a[rs][2 * u + 1] = v.y;
-        }
-    } else {
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
+        for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
           for (int rs = 0; rs < 4; ++rs) {
-            const int gr = r0 + 16 * rs + li, gc = c0 + 8 * u + 2 * lq + e;
-            a[rs][2 * u + e] = (gr < m && gc < m) ? (gr >= gc ? A[(size_t)gc * lda + gr] : A[(size_t)gr * lda + gc]) : 0.0;
+            const double2 v = *reinterpret_cast<const double2*>(A + (size_t)(r0 + 16 * rs + li) * lda + c0 +
+                                                                8 * (4 * hf + uu) + 2 * lq);
+            a[rs][2 * uu] = v.x;
+            a[rs][2 * uu + 1] = v.y;
           }
-    }
+      } else {
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+        for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int gc = c0 + 8 * u + 2 * lq + e;
+          for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int cs = 0; cs < 2; ++cs) b[cs][2 * u + e] = gc < m ? Vt[(size_t)gc * kB + 16 * cs + li] : 0.0;
+            for (int rs = 0; rs < 4; ++rs) {
+              const int gr = r0 + 16 * rs + li, gc = c0 + 8 * (4 * hf + uu) + 2 * lq + e;
+              a[rs][2 * uu + e] =
+                  (gr < m && gc < m) ? (gr >= gc ? A[(size_t)gc * lda + gr] : A[(size_t)gr * lda + gc]) : 0.0;
+            }
       }
 #pragma unroll
-    for (int st = 0; st < 16; ++st)
+      for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
-      for (int rs = 0; rs < 4; ++rs)
+        for (int e = 0; e < 2; ++e) {
+          const int gc = c0 + 8 * (4 * hf + uu) + 2 * lq + e;
 #pragma unroll
-        for (int cs = 0; cs < 2; ++cs) acc[rs][cs] = mfma64(a[rs][st], b[cs][st], acc[rs][cs]);
+          for (int cs = 0; cs < 2; ++cs) b[cs][2 * uu + e] = gc < m ? Vt[(size_t)gc * kB + 16 * cs + li] : 0.0;
+        }
+#pragma unroll
+      for (int st = 0; st < 8; ++st)
+#pragma unroll
+        for (int rs = 0; rs < 4; ++rs)
+#pragma unroll
+          for (int cs = 0; cs < 2; ++cs) acc[rs][cs] = mfma64(a[rs][st], b[cs][st], acc[rs][cs]);
+    }
   }
   // D(row (lane >> 4) + 4 x, col lane & 15) of output tile (rs, cs) = Y(16 rs + row, 16 cs + col)
   for (int ww = 0; ww < 4; ++ww) {
