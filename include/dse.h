@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 11
+#define DSE_ABI_VERSION 12
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -112,7 +112,10 @@ typedef struct dse_stats {
   double matrix_products;     /* (k_symv + k_symv_reduce, or zgemv), their count, and the        */
   double matrix_bytes_per_product; /* bytes one product reads (U's stored tiles + x; ABI 10)     */
   int32_t real_problems;      /* registers run as two real recurrences in the rotated frame      */
-  int32_t reserved1;          /* (k_real, option "real"; ABI 11)                                 */
+                              /* (k_real, option "real"; ABI 11)                                 */
+  int32_t eig_fallbacks;      /* dense registers whose two-stage eigensolve gave up a bounded     */
+                              /* cross-workgroup poll and were re-solved by rocSOLVER dsyevd     */
+                              /* (option "eig_spin_limit"; ABI 12)                                */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -203,6 +206,10 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         qubits and all their tiles fit the chip at once, else none; 0 never
  *          "span"         the same with a fixed number s = 1..4 of top bits per register
  *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
+ *          "eig_spin_limit"  two-stage eigensolver: rounds a poll of another workgroup's result
+ *                         waits before it gives up (default 2^22, ~0.1 s); a give-up voids that
+ *                         solve and the register is re-solved by rocSOLVER dsyevd (stats
+ *                         eig_fallbacks); -1: every solve gives up at once (tests)
  *          "dense_refine" dense engine: 1 (default) eigenvalues refined by double-double
  *                         Rayleigh quotients (exact diagonal) and output phases reduced modulo
  *                         2 pi in double-double; 0 the eigensolver's values and fp64 phases */

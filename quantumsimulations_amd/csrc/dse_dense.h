@@ -93,17 +93,24 @@ int eig_sym_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, d
 // (ormtr_lower, offset 32).  work: eig2_workspace(n) bytes (the chase's reflectors: ~n^2 / 2
 // doubles); n_cu: compute units (the chase's workgroups are co-resident)
 size_t eig2_workspace(int n);
-// Q2 application variant (probe A/B; dse_eig2.hip g_q2_variant)
+#ifdef DSE_EIG2_VARIANTS
+// A/B variants (probe builds only: tools/probe_eig2.cpp; dse_eig2.hip g_q2_variant, ...)
 void set_eig2_q2_variant(int v);
 void set_eig2_chase_variant(int v);
 void set_eig2_syr2k_tri(int v);
-int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work);
+#endif
+// spin: rounds a cross-workgroup poll waits before it gives up (option eig_spin_limit; < 0: fail at
+// once, tests).  A give-up makes sb2st_lower / eig_sym_2stage return kEig2PollTimeout (the band or
+// tridiagonal is then void; the dense engine re-solves the register with rocSOLVER dsyevd).
+constexpr int kEig2PollTimeout = -9;
+constexpr int kEig2DefaultSpin = 1 << 22;
+int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work, int spin = kEig2DefaultSpin);
 int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu,
-                long long* dbg = nullptr);
+                int spin = kEig2DefaultSpin, long long* dbg = nullptr);
 int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work);
 int eig2_q1(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, double* Z, int ldz, void* work);
 int eig_sym_2stage(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
-                   double* e, void* work, int* info, int n_cu);
+                   double* e, void* work, int* info, int n_cu, int spin = kEig2DefaultSpin);
 
 }  // namespace dse
 

@@ -65,6 +65,12 @@ k_dense_h(const DenseProb* __restrict__ probs, int dim) {
 }
 
 // ---- double-double arithmetic (value = hi + lo, |lo| <= ulp(hi) / 2) ----
+// No FMA contraction from here to the end of k_dense_phase: HIP compiles with -ffp-contract=fast,
+// and a contracted p.hi + p.lo (p.hi = a * b) is fma(a, b, p.lo), which counts the product's
+// rounding error twice -- every double-double product then carries an fp64-sized error, and the
+// refined eigenvalues were no better than ~eps |H| (round 4's 1.3e-8 at 30 s; 1e-13 without it).
+// The explicit fma() calls below are the intended ones.
+#pragma clang fp contract(off)
 struct ddv {
   double hi, lo;
 };
@@ -183,6 +189,7 @@ k_dense_phase(const DenseProb* __restrict__ probs, int dim, const double* __rest
   blk[a + (size_t)j * dim] = c * co;
   blk[a + (size_t)(tb + j) * dim] = -c * s;
 }
+#pragma clang fp contract(fast)
 
 // block sum of 7 values (256 threads = 4 waves)
 __device__ __forceinline__ void block_sum7(double* v, double (*red)[8]) {

@@ -75,15 +75,30 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int e, double v
 // + k]) and pivot row (piv[j kB + k]) are written once each (sc1) into slots that hold the
 // all-ones sentinel before the launch; every workgroup polls the values themselves (a slot still
 // holding the sentinel is read again), so a column costs one store-to-load round trip and no
-// barrier (the mailbox form of the chase; the polls give up after ~2^22 rounds, never hanging on a
-// NaN input).
+// barrier (the mailbox form of the chase).
+//
+// Every cross-workgroup poll of this file (here and in the chase) is bounded: after `spin` rounds
+// (option eig_spin_limit) a poll gives up and sets the solve's device error word *err, and every
+// other poll that finds the word set gives up at once, so a launch whose workgroups are not all
+// resident (or a NaN input, whose all-ones payload is the sentinel) drains instead of hanging.  The
+// host reads the word after the chase (sb2st_lower -> kEig2PollTimeout) and the dense engine
+// re-solves that register with rocSOLVER dsyevd.  spin < 0 sets the word at the start (tests).
 constexpr unsigned long long kSentinel = ~0ull;
 __device__ __forceinline__ bool is_sentinel(double v) {
   return __builtin_bit_cast(unsigned long long, v) == kSentinel;
 }
+// a poll that has missed `it` times gives up: the limit, or another poll's give-up (checked on the
+// first miss and every 64th after); a give-up is recorded in *err (vector atomic)
+__device__ __forceinline__ bool poll_give_up(int* err, int spin, int it) {
+  bool up = it >= spin;
+  if (!up && (it & 63) == 0) up = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (up) __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return up;
+}
 __global__ void __launch_bounds__(kPanelRows)
 k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
-           double* __restrict__ piv, double* __restrict__ Vw, double* __restrict__ Vt) {
+           double* __restrict__ piv, double* __restrict__ Vw, double* __restrict__ Vt, int* __restrict__ err,
+           int spin) {
   __shared__ double red[kPanelRows / 64][kB];
   __shared__ double red8[8][kB];
   __shared__ double tot[kB];
@@ -94,6 +109,7 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
   const __amdgpu_buffer_rsrc_t vrs = ptr_rsrc(piv, (size_t)kB * kB * 8);
   const int r = blockIdx.x * kPanelRows + tid;
   const bool own = r < m;
+  if (spin < 0 && blockIdx.x == 0 && tid == 0) __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double x[kB];
 #pragma unroll
   for (int k = 0; k < kB; ++k) x[k] = own ? P[(size_t)k * lda + r] : 0.0;
@@ -139,11 +155,11 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
 #pragma unroll
       for (int q = 0; q < 16; ++q) pv[q] = live(q) ? bload(prs, slot(q)) : 0.0;
       double pr = tid < kB && tid >= j ? bload(vrs, j * kB + tid) : 0.0;
-      for (int it = 0; it < (1 << 22); ++it) {
+      for (int it = 0;; ++it) {
         bool miss = is_sentinel(pr);
 #pragma unroll
         for (int q = 0; q < 16; ++q) miss |= is_sentinel(pv[q]);
-        if (!miss) break;
+        if (!miss || poll_give_up(err, spin, it)) break;
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int q = 0; q < 16; ++q)
@@ -574,6 +590,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t band_rsrc(double* S, int n) {
 // store of the band sc1, each storing wave's s_waitcnt vmcnt(0) before its sc1 flag store, the
 // consumer wave polls the flag with sc1 loads and then loads)
 
+constexpr int kChaseWG = 4;  // waves per chase workgroup
+
 struct ChaseVec {
   double x[kB];
   double v[kB];
@@ -582,6 +600,10 @@ struct ChaseVec {
   double Dt[kB][kB + 1];  // (lane = column); pitch kB + 1: both conflict-free
 };
 
+#ifdef DSE_EIG2_VARIANTS
+// ---- A/B record (tools/probe_eig2.cpp builds with -DDSE_EIG2_VARIANTS; not in libdse.so): the
+// round-4 chase that waits for task (s - 1, t + 2) complete (variant 0, 336 ms at 2^14) and its
+// per-task timing build (DBG, option EIG2_CHASE_DBG of the probe).  Its polls are unbounded.
 __device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 
 template <bool DBG>
@@ -715,7 +737,6 @@ __device__ void chase_task(double* __restrict__ S, int n, int s, int t, ChaseVec
 // prog[s] = tasks of sweep s done (zeroed before); relaxed agent-scope (sc1) flag stores and polls.
 // DBG: per worker, the sums of the poll wait, load, compute + store issue and store drain times
 // (100 MHz ticks) and the task count into dbg[5 w ..].
-constexpr int kChaseWG = 4;  // waves per chase workgroup
 template <bool DBG>
 __global__ void __launch_bounds__(64 * kChaseWG)
 k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long long* __restrict__ goff,
@@ -763,6 +784,7 @@ k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long lon
     }
   }
 }
+#endif  // DSE_EIG2_VARIANTS
 
 // The chase with the next task's operands prefetched (round 4, default).  Task (s, t)'s R block is
 // its next task's L block: it stays in registers (stored there, as L), so a task loads only D and R,
@@ -777,7 +799,7 @@ k_sb2st(double* __restrict__ S, int n, double* __restrict__ refl, const long lon
 template <bool EARLY>
 __global__ void __launch_bounds__(64 * kChaseWG)
 k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long long* __restrict__ goff,
-           int* __restrict__ prog, unsigned long long* __restrict__ mb, int MT) {
+           int* __restrict__ prog, unsigned long long* __restrict__ mb, int MT, int* __restrict__ err, int spin) {
   __shared__ ChaseVec lds[kChaseWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = gridDim.x * kChaseWG, w = blockIdx.x * kChaseWG + wv;
@@ -787,10 +809,12 @@ k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long 
   for (int s = w; s < n - 1; s += W) {
     const int nt = chase_tasks(n, s);
     const int ntp = s > 0 ? chase_tasks(n, s - 1) : 0;
-    auto wait_prog = [&](int need) {
+    auto wait_prog = [&](int need) {  // bounded (poll_give_up): a give-up drains the launch
       if (s > 0)
-        while (__hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+        for (int it = 0; __hip_atomic_load(prog + s - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need; ++it) {
+          if (poll_give_up(err, spin, it)) break;
           __builtin_amdgcn_s_sleep(1);
+        }
     };
     double Lcar[16], Dm[16], Rm[16];  // carried L (R layout: lane = row), D (memory layout), R
     auto load_dr = [&](int t) {
@@ -828,9 +852,9 @@ k_sb2st_pf(double* __restrict__ S, int n, double* __restrict__ refl, const long 
       // R(b-1, b-1) from task (s - 1, t + 2)
       if (s > 0 && mr == kB) {
         unsigned long long bits;
-        for (int it = 0; it < (1 << 24); ++it) {  // bounded: never hangs on a NaN (sentinel) value
+        for (int it = 0;; ++it) {  // bounded: a NaN beta is the sentinel; a give-up drains the launch
           bits = __hip_atomic_load(mb + (size_t)(s - 1) * MT + t + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (bits != ~0ull) break;
+          if (bits != ~0ull || poll_give_up(err, spin, it)) break;
           __builtin_amdgcn_s_sleep(1);
         }
         if (j == kB - 1 && h == 1) Rm[15] = __builtin_bit_cast(double, bits);
@@ -958,7 +982,7 @@ __global__ void k_sb_tridiag(const double* __restrict__ S, int n, double* __rest
 // word and an acquire fence after the poll (the memory model's own workgroup hand-off).
 constexpr int kQ2Rec = kQ2NB * kRec;             // doubles per group
 constexpr int kQ2PerLane = (kQ2Rec + 63) / 64;    // staging loads per lane
-constexpr int kQ2Waves = 4;
+[[maybe_unused]] constexpr int kQ2Waves = 4;  // (probe variants)
 // NC columns per lane (64 NC per workgroup): each reflector value read from LDS serves 2 NC FMAs.
 // PF: group t + 1's new rows are loaded under group t (and released one group late); PAIR: two
 // reflectors per step (both dot products on one window).
@@ -1227,7 +1251,9 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
   }
 }
 
-// k_sb_q2 variant (set_eig2_q2_variant; 2^14, profiles/r04/eig2_q2_variants.txt): 0 one
+#ifdef DSE_EIG2_VARIANTS
+// A/B record, probe builds only (tools/probe_eig2.cpp, -DDSE_EIG2_VARIANTS); libdse.so runs the
+// defaults as constants.  k_sb_q2 variant (2^14, profiles/r04/eig2_q2_variants.txt): 0 one
 // reflector at a time, rows loaded after each group (346 ms); 1 pairs + the next rows under the
 // group (361); 2 two columns per lane (649); 3 pairs (357); 4 = 0 with the records copied global ->
 // LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default); 6 / 7 the reflector values
@@ -1240,6 +1266,9 @@ int g_chase_variant = 1;
 // the trailing update's grid: 0 2-D (nbk x nbk, the upper tiles idle; default), 1 1-D over the lower
 // tiles (band 413-425 vs 377 ms at 2^14: the 2-D order, I fastest, keeps a column's V/W rows warm)
 int g_syr2k_tri = 0;
+#else
+constexpr int g_q2_variant = 5, g_chase_variant = 1, g_syr2k_tri = 0;
+#endif
 
 struct Eig2Ws {
   double* tau1;     // n: stage-1 reflectors (zero where none)
@@ -1263,6 +1292,7 @@ struct Eig2Ws {
   int* prog;        // n
   unsigned long long* mb;  // n x (chase_tasks(n, 0) + 1): the chase's mailboxes
   int* cnt;         // 1
+  int* err;         // 1: a bounded poll gave up (poll_give_up)
 };
 
 // doubles of the group-major reflector records: per block of kQ2NB sweeps, chase_tasks(first
@@ -1313,15 +1343,18 @@ Eig2Ws carve2(void* work, int n, size_t* bytes = nullptr) {
   w.prog = (int*)take((size_t)n * 4);
   w.mb = (unsigned long long*)take((size_t)n * (chase_tasks(n, 0) + 1) * 8);
   w.cnt = (int*)take(256);
+  w.err = (int*)take(256);
   if (bytes) *bytes = off;
   return w;
 }
 
 }  // namespace
 
+#ifdef DSE_EIG2_VARIANTS
 void set_eig2_q2_variant(int v) { g_q2_variant = v; }
 void set_eig2_chase_variant(int v) { g_chase_variant = v; }
 void set_eig2_syr2k_tri(int v) { g_syr2k_tri = v; }
+#endif
 
 size_t eig2_workspace(int n) {
   size_t b = 0;
@@ -1333,11 +1366,12 @@ size_t eig2_workspace(int n) {
 // update: the update first rewrites A22's first kB columns (the next panel and its diagonal block),
 // then the rest while the panel is factored; V, its copies and the V^T V partials are double-buffered
 // by panel parity.
-int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work) {
+int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, void* work, int spin) {
   (void)h;
   Eig2Ws ws = carve2(work, n);
   if (hipMemsetAsync(ws.tau1, 0, (size_t)n * 8, st) != hipSuccess) return -1;
   if (hipMemsetAsync(ws.cnt, 0, sizeof(int), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(ws.err, 0, sizeof(int), st) != hipSuccess) return -1;
   hipStream_t s2 = nullptr;
   hipEvent_t evS = nullptr, evP = nullptr;
   if (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
@@ -1352,7 +1386,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     if (G > 128) return -2;
     if (hipMemsetAsync(ws.part, 0xff, ((size_t)kB * G * (kB + 1) + (size_t)kB * kB) * 8, q) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_panel_qr, dim3(G), dim3(kPanelRows), 0, q, P, lda, m, ws.tau1 + i, ws.part,
-                       ws.part + (size_t)kB * G * (kB + 1), ws.Vw2[par], ws.Vt2[par]);
+                       ws.part + (size_t)kB * G * (kB + 1), ws.Vw2[par], ws.Vt2[par], ws.err, spin);
     hipLaunchKernelGGL(k_sb_vty, dim3(ng), dim3(256), 0, q, ws.Vw2[par], ws.Vw2[par], m, ws.part2v);
     hipLaunchKernelGGL(k_sb_tmat, dim3(1), dim3(kB * kB), 0, q, ws.part2v, ng, k, ws.tau1 + i,
                        ws.T + (size_t)p * kB * kB);
@@ -1403,7 +1437,7 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
 }
 
 int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, double* e, void* work, int n_cu,
-                long long* dbg) {
+                int spin, long long* dbg) {
   Eig2Ws ws = carve2(work, n);
   std::vector<long long> goff;
   const size_t nrefl = chase_refl_doubles(n, &goff);
@@ -1413,30 +1447,47 @@ int sb2st_lower(hipStream_t st, int n, const double* A, int lda, double* d, doub
   hipLaunchKernelGGL(k_sb_band, dim3((unsigned)(((size_t)n * kLD + 255) / 256)), dim3(256), 0, st, A, lda, n, ws.S);
   // ~n / (3 b) sweeps run at once: one worker per 2 b columns, at most one workgroup per CU
   const int nwg = std::max(1, std::min(n_cu, (n + 2 * kB * kChaseWG - 1) / (2 * kB * kChaseWG)));
+#ifdef DSE_EIG2_VARIANTS
   if (dbg)
     hipLaunchKernelGGL(k_sb2st<true>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, dbg);
   else if (g_chase_variant == 0)
     hipLaunchKernelGGL(k_sb2st<false>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, dbg);
-  else {
+  else
+#else
+  (void)dbg;
+#endif
+  {
     const int MT = chase_tasks(n, 0) + 1;
     if (hipMemsetAsync(ws.mb, 0xff, (size_t)n * MT * 8, st) != hipSuccess) return -1;
     if (g_chase_variant == 2)
-      hipLaunchKernelGGL(k_sb2st_pf<true>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb, MT);
+      hipLaunchKernelGGL(k_sb2st_pf<true>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb,
+                         MT, ws.err, spin);
     else
-      hipLaunchKernelGGL(k_sb2st_pf<false>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb, MT);
+      hipLaunchKernelGGL(k_sb2st_pf<false>, dim3(nwg), dim3(64 * kChaseWG), 0, st, ws.S, n, ws.refl, ws.goff, ws.prog, ws.mb,
+                         MT, ws.err, spin);
   }
   hipLaunchKernelGGL(k_sb_tridiag, dim3((n + 255) / 256), dim3(256), 0, st, ws.S, n, d, e);
   if (hipStreamSynchronize(st) != hipSuccess) return -1;  // goff is host memory until here
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  if (hipGetLastError() != hipSuccess) return -1;
+  int herr = 0;  // a bounded poll of the panel QR or of the chase gave up: the band / tridiagonal is void
+  if (hipMemcpy(&herr, ws.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return herr ? kEig2PollTimeout : 0;
 }
 
 int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
+#ifndef DSE_EIG2_VARIANTS
+  static_assert(g_q2_variant == 5, "libdse.so: k_sb_q2<1, false, false, true, 8> only");
+#endif
   Eig2Ws ws = carve2(work, n);
   const dim3 tg((n + 63) / 64, (n + 63) / 64);
   const size_t nrec = chase_refl_doubles(n) / kRec;
   hipLaunchKernelGGL(k_sb_q2c, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, st, ws.refl, nrec);
   hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, Z, ldz, ws.Zt, n, n);
-  const dim3 g1((n + 63) / 64), blk(64 * kQ2Waves);
+  const dim3 g1((n + 63) / 64);
+#ifndef DSE_EIG2_VARIANTS
+  hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 8>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff);
+#else
+  const dim3 blk(64 * kQ2Waves);
   switch (g_q2_variant) {
     case 1: hipLaunchKernelGGL((k_sb_q2<1, true, true, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 2: hipLaunchKernelGGL((k_sb_q2<2, false, false, false, 4>), dim3((n + 127) / 128), blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
@@ -1447,6 +1498,7 @@ int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
     case 7: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4, true>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     default: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
   }
+#endif
   // back: Z(r, c) = Zt[r n + c], i.e. the column-major read of Zt^T
   hipLaunchKernelGGL(k_sb_transpose, tg, dim3(256), 0, st, ws.Zt, n, Z, ldz, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1458,10 +1510,10 @@ int eig2_q1(rocblas_handle h, hipStream_t st, int n, const double* A, int lda, d
 }
 
 int eig_sym_2stage(rocblas_handle h, hipStream_t st, int n, double* A, int lda, double* lam, double* V, int ldv,
-                   double* e, void* work, int* info, int n_cu) {
-  int rc = sy2sb_lower(h, st, n, A, lda, work);
+                   double* e, void* work, int* info, int n_cu, int spin) {
+  int rc = sy2sb_lower(h, st, n, A, lda, work, spin);
   if (rc) return rc;
-  if ((rc = sb2st_lower(st, n, A, lda, lam, e, work, n_cu, nullptr))) return rc;
+  if ((rc = sb2st_lower(st, n, A, lda, lam, e, work, n_cu, spin, nullptr))) return rc;
   if (rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, ldv, info) != rocblas_status_success) return -8;
   if ((rc = q2_apply(st, n, V, ldv, work))) return rc;
   return eig2_q1(h, st, n, A, lda, V, ldv, work);

@@ -272,6 +272,10 @@ struct dse_ctx {
   // half-matrix tridiagonalisation from 2^13, rocSOLVER dstedc, the blocked back-transformation)
   // from kEigHalfMinDim amplitudes, dsyevd below; 2 eig_sym_lower from 2^10 (tests)
   int eig_impl = 1;
+  // the two-stage eigensolver's cross-workgroup polls give up after this many rounds (option
+  // eig_spin_limit; < 0: at once, tests); a give-up re-solves that register with dsyevd
+  int eig_spin = kEig2DefaultSpin;
+  std::atomic<int> eig_fallbacks{0};  // registers re-solved that way in the last evolve
   // dense engine: eigenvalues refined by double-double Rayleigh quotients and output phases reduced
   // in double-double (option "dense_refine", default 1; 0: the eigensolver's eigenvalues and fp64
   // phases, whose error grows like eps |lambda| t: ~1e-8 at the reference grid's 30 s)
@@ -1360,6 +1364,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
                                  // 3 two-stage from 2^10
     if (!(value >= 0 && value <= 3)) return fail(ctx, DSE_ERR_ARG, "eig_impl must be 0, 1, 2 or 3");
     ctx->eig_impl = (int)value;
+  } else if (k == "eig_spin_limit") {  // two-stage eigensolver: poll rounds before a give-up (< 0: at once)
+    if (!(value >= -1 && value <= 1 << 30)) return fail(ctx, DSE_ERR_ARG, "eig_spin_limit must be in -1..2^30");
+    ctx->eig_spin = (int)value;
   } else if (k == "dense_refine") {  // dense engine: refined eigenvalues + double-double phases
     ctx->dense_refine = value != 0.0;
   } else if (k == "symv_fused") {  // matrix mode: each product's reduction in the product's launch
@@ -2095,9 +2102,19 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           double* Vi = J.V + J.dim * J.dim * i;
           werr[w] = hipMemcpyAsync(scr[w].A, Vi, J.dim * J.dim * sizeof(double), hipMemcpyDeviceToDevice,
                                    ctx->eig_st[w]);
-          if (werr[w] == hipSuccess && J.dim >= two_min)
+          if (werr[w] == hipSuccess && J.dim >= two_min) {
             wrc[w] = eig_sym_2stage(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
-                                    J.E + J.dim * i, scr[w].work, J.info + i, ctx->n_cu);
+                                    J.E + J.dim * i, scr[w].work, J.info + i, ctx->n_cu, ctx->eig_spin);
+            if (wrc[w] == kEig2PollTimeout) {  // a poll gave up (workgroups not co-resident): H' again, dsyevd
+              ctx->eig_fallbacks++;
+              wrc[w] = 0;
+              werr[w] = hipMemsetAsync(Vi, 0, J.dim * J.dim * sizeof(double), ctx->eig_st[w]);
+              if (werr[w] == hipSuccess) werr[w] = launch_dense_h(J.d_desc + i, 1, (int)J.dim, ctx->eig_st[w]);
+              if (werr[w] == hipSuccess)
+                wst[w] = rocsolver_dsyevd(ctx->eig_h[w], rocblas_evect_original, rocblas_fill_upper, dim, Vi, dim,
+                                          J.lam + J.dim * i, J.E + J.dim * i, J.info + i);
+            }
+          }
           else if (werr[w] == hipSuccess)
             wrc[w] = eig_sym_lower(ctx->eig_h[w], ctx->eig_st[w], dim, scr[w].A, dim, J.lam + J.dim * i, Vi, dim,
                                    J.E + J.dim * i, scr[w].tau, scr[w].work, J.info + i);
@@ -3289,6 +3306,9 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     std::vector<BasisInit> init;
     uint64_t max_amps = 0;
     for (auto& P : ctx->probs) {
+      // the re-run after a hand-off timeout keeps the dense registers' first-pass results, whose
+      // final state k_dense_final wrote into buf[0]
+      if (ctx->rerun && P.dn) continue;
       BasisInit e;
       e.ptr = P.buf[0];
       e.n = uint64_t(1) << P.n_local;
@@ -3573,6 +3593,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     int n_real = 0;
     for (auto& P : ctx->probs) n_real += P.rl ? 1 : 0;
     stats->real_problems = n_real;
+    stats->eig_fallbacks = ctx->eig_fallbacks.load();
     stats->dense_ms = dense_ms;
     stats->dense_eig_ms = dense_eig_ms;
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
@@ -3607,6 +3628,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
 int dse_evolve(dse_ctx* ctx, const double* t, int n_t, double tol, double* obs_out, dse_stats* stats) {
   if (!ctx) return DSE_ERR_ARG;
   ctx->handoff_fallbacks = 0;
+  ctx->eig_fallbacks = 0;
   int rc = evolve_impl(ctx, t, n_t, tol, obs_out, stats);
   int* const d_err = ctx->d_err_cur;
   ctx->d_err_cur = nullptr;

@@ -2,7 +2,8 @@
 
 Run ONLY in the build container (it reads /root/reference, which the GPU box does not have):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_n14.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_n14.py            (200 us grid)
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_n14.py --bench    (bench grid, ~15 min)
 
 Same route as make_golden.py: the reference's ``dipolar_ensemble_with_rare.py`` is imported by
 path with the QuTiP stand-in (``_qutip_standin``, scipy.sparse-backed) first on sys.path, so H,
@@ -29,6 +30,10 @@ the series) and stores the largest difference as <v>_<d>_cross_check (2e-13 to 1
 <v>_<d>_expm_diff.  expm_multiply over the whole grid in one call is NOT used: at alpha t ~ 1e3 it
 drifts to 1e-11 here, with a norm error of 1e-12, while both Chebyshev runs keep the norm to
 1e-14.
+
+With --bench: hpsi_traces_n14_bench.npz, the same traces (no H @ v) on bench.py's whole config-3
+grid, t = linspace(0, 1e-3, 101) (1 ms, 101 outputs), for the same 9 (variant, delta) cases; the
+cases run in parallel worker processes.
 """
 from __future__ import annotations
 
@@ -52,6 +57,7 @@ VARIANTS = mg.VARIANTS
 OBS = mg.OBS
 DELTAS = (0.0, 75000.0, 150000.0)
 T = np.linspace(0.0, 2e-4, 21)
+T_BENCH = np.linspace(0.0, 1e-3, 101)   # bench.py's config-3 grid (1 ms, 101 outputs)
 
 
 def gershgorin(Hc: sp.csr_matrix):
@@ -94,40 +100,60 @@ def expect(states: np.ndarray, op) -> np.ndarray:
     return np.real(np.einsum("td,td->t", states.conj(), (op @ states.T).T))
 
 
+def one_case(v: str, dlt: float, t: np.ndarray, with_hv: bool):
+    p = mg.sweep_params(13, dlt, v, float(t[-1]), len(t))
+    H, eops = ref.build_hamiltonian_rare(p)
+    Hc = H.data.tocsr()
+    psi0 = ref.initial_state_rare(p).full().ravel()
+    key = f"{v}_{int(dlt)}"
+    out = {}
+    if with_hv:
+        vec = mg.rand_state(Hc.shape[0], 1400)
+        out[f"{key}_Hv"] = Hc @ vec
+        for k in OBS:
+            out[f"{key}_expect_{k}"] = float(np.real(np.vdot(vec, eops[k].data @ vec)))
+    out[f"{key}_psi0_index"] = int(np.argmax(np.abs(psi0)))
+    st = chebyshev_trace(Hc, psi0, t, gershgorin(Hc))
+    ch = chebyshev_trace(Hc, psi0, t, eig_bounds(Hc))
+    ex = [psi0.astype(complex)]
+    for m in range(1, len(t)):
+        ex.append(expm_multiply(-1j * (t[m] - t[m - 1]) * Hc, ex[-1]))
+    ex = np.array(ex)
+    cross = dexp = 0.0
+    for k in OBS:
+        a = expect(st, eops[k].data)
+        cross = max(cross, float(np.max(np.abs(a - expect(ch, eops[k].data)))))
+        dexp = max(dexp, float(np.max(np.abs(a - expect(ex, eops[k].data)))))
+        out[f"{key}_{k}"] = a
+    out[f"{key}_state_norm"] = np.linalg.norm(st, axis=1)
+    out[f"{key}_cross_check"] = cross
+    out[f"{key}_expm_diff"] = dexp
+    print(f"{key}: dim {Hc.shape[0]}, nnz {Hc.nnz}, Chebyshev(Gershgorin) vs "
+          f"Chebyshev(eigsh) {cross:.2e}, vs expm_multiply per interval {dexp:.2e}", flush=True)
+    assert cross < 5e-12, cross
+    return out
+
+
+def _case(args):
+    return one_case(*args)
+
+
 def main():
     t0 = time.time()
-    out = {"t": T}
-    for v in VARIANTS:
-        for dlt in DELTAS:
-            p = mg.sweep_params(13, dlt, v, float(T[-1]), len(T))
-            H, eops = ref.build_hamiltonian_rare(p)
-            Hc = H.data.tocsr()
-            psi0 = ref.initial_state_rare(p).full().ravel()
-            key = f"{v}_{int(dlt)}"
-            vec = mg.rand_state(Hc.shape[0], 1400)
-            out[f"{key}_Hv"] = Hc @ vec
-            out[f"{key}_psi0_index"] = int(np.argmax(np.abs(psi0)))
-            for k in OBS:
-                out[f"{key}_expect_{k}"] = float(np.real(np.vdot(vec, eops[k].data @ vec)))
-            st = chebyshev_trace(Hc, psi0, T, gershgorin(Hc))
-            ch = chebyshev_trace(Hc, psi0, T, eig_bounds(Hc))
-            ex = [psi0.astype(complex)]
-            for m in range(1, len(T)):
-                ex.append(expm_multiply(-1j * (T[m] - T[m - 1]) * Hc, ex[-1]))
-            ex = np.array(ex)
-            cross = dexp = 0.0
-            for k in OBS:
-                a = expect(st, eops[k].data)
-                cross = max(cross, float(np.max(np.abs(a - expect(ch, eops[k].data)))))
-                dexp = max(dexp, float(np.max(np.abs(a - expect(ex, eops[k].data)))))
-                out[f"{key}_{k}"] = a
-            out[f"{key}_state_norm"] = np.linalg.norm(st, axis=1)
-            out[f"{key}_cross_check"] = cross
-            out[f"{key}_expm_diff"] = dexp
-            print(f"{key}: dim {Hc.shape[0]}, nnz {Hc.nnz}, Chebyshev(Gershgorin) vs "
-                  f"Chebyshev(eigsh) {cross:.2e}, vs expm_multiply per interval {dexp:.2e}", flush=True)
-            assert cross < 5e-12, cross
-    np.savez(os.path.join(HERE, "hpsi_traces_n14.npz"), **out)
+    bench = "--bench" in sys.argv
+    t = T_BENCH if bench else T
+    out = {"t": t}
+    cases = [(v, dlt, t, not bench) for v in VARIANTS for dlt in DELTAS]
+    if bench:
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(max_workers=min(len(cases), os.cpu_count() or 1)) as ex:
+            for o in ex.map(_case, cases):
+                out.update(o)
+    else:
+        for c in cases:
+            out.update(one_case(*c))
+    name = "hpsi_traces_n14_bench.npz" if bench else "hpsi_traces_n14.npz"
+    np.savez(os.path.join(HERE, name), **out)
     print(f"done in {time.time() - t0:.1f} s")
 
 

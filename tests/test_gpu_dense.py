@@ -10,8 +10,10 @@ output time exact from one GEMM (rocBLAS dgemm) and the observable pass.
 * the reference's default workload (n_sea = 6, 13 detunings x 3 variants, 30 s / 20 000 outputs,
   sweep_sea_detuning.py:1223-1240) goes to the dense engine by the cost model (option dense = 1)
   and its first outputs agree with the Chebyshev engine on the same grid prefix; its norms stay 1
-* N = 14 on the whole 30 s grid against the Chebyshev kernels over its first 100 intervals: the
-  difference and its fitted growth within the stated fp64 floor 1e-10 + 1.5 eps ||H|| t
+* N = 14 on the whole 30 s grid against the Chebyshev kernels over its first 100 intervals (within
+  the Chebyshev engine's own fp64 drift, 1e-10 + 1.5 eps ||H|| t), and the whole grid to t = 30 s
+  through two independent eigensolvers (the two-stage one and rocSOLVER dsyevd): their
+  eigenvector rounding differs, so an error that grew with t would show as a growing difference
 * the cost model keeps the 1 ms N = 14 grid on the Chebyshev kernels
 * the half-matrix eigensolver (csrc/dse_sytrd.hip, option eig_impl): config 2 through it at dim 4096
   against the exact fixture (1e-10) and against rocSOLVER dsyevd (1e-11); an N = 13 register (dim
@@ -125,12 +127,12 @@ def test_cost_model_keeps_short_n14_grid_on_chebyshev(engine):
 def test_dense_full_grid_n14_matches_chebyshev_prefix(engine):
     """BASELINE's "(full sweep)" engine at config 3's size: the dense engine on the WHOLE reference
     grid (30 s, 20 000 outputs; dim 16384 / 8192 eigendecompositions) for the 3 variants at 150 kHz
-    against the persistent Chebyshev kernels (an exact propagator to the 1e-14 truncation per
-    interval) over the grid's first 100 intervals (0.15 s).  The difference grows like the fp64
-    eigenvector floor, |d<O>(t)| <= 1e-10 + 1.5 eps ||H|| t (test_gpu_grid30.py, pinned at N = 7
-    by the mpmath fixture), with ||H|| <= the Gershgorin bound of problem.spectral_bounds; the
-    fitted growth rate extrapolates to the stated tolerance at 30 s (bench
-    full_sweep.tolerance_at_t_final)."""
+    against the persistent Chebyshev kernels over the grid's first 100 intervals (0.15 s).  Each
+    Chebyshev interval is exact to its 1e-14 truncation, but its ~1e4 fp64 H applications are the
+    exact evolution of an H perturbed by ~eps ||H||, so the Chebyshev trace itself drifts like
+    eps ||H|| t (the dense engine's refined eigenvalues do not: test_gpu_grid30.py pins it at 1e-12
+    to 30 s at N = 7, and test_dense_30s_n14_two_eigensolvers_agree at N = 14): the difference is
+    held to 1e-10 + 1.5 eps ||H|| t and its growth rate recorded."""
     t_ref = np.linspace(0.0, 30.0, 20000)
     params = [sweep_point_params(13, 150e3, v, 30.0, 20000) for v in VARIANTS]
     probs = [pb.build_problem(p) for p in params]
@@ -150,22 +152,41 @@ def test_dense_full_grid_n14_matches_chebyshev_prefix(engine):
     tk = t_ref[1:K + 1]
     err = np.max(np.abs(obs[:, :6, 1:K + 1] - ch[:, :6, 1:]), axis=(0, 1))
     hnorm = max(max(abs(a) for a in pb.spectral_bounds(p)) for p in probs)
-    eps = np.finfo(float).eps
-    bound = 1e-10 + 1.5 * eps * hnorm * tk
     slope_ls = float(np.sum(err * tk) / np.sum(tk * tk))   # least-squares rate through the origin
     slope_env = float(np.max(err[9:] / tk[9:]))             # envelope rate past the first 10 outputs
     print(f"N=14 dense vs Chebyshev over {K} intervals: max {err.max():.2e} at t = {tk[np.argmax(err)]:.3f} s; "
           f"rate LS {slope_ls:.2e}/s, envelope {slope_env:.2e}/s -> at 30 s {slope_ls * 30:.2e} / "
-          f"{slope_env * 30:.2e}; stated 1e-10 + 1.5 eps ||H|| t = {1e-10 + 1.5 * eps * hnorm * 30:.2e} "
-          f"(||H|| <= {hnorm:.3e} rad/s)")
+          f"{slope_env * 30:.2e} (||H|| <= {hnorm:.3e} rad/s)")
     rec_dir = os.environ.get("DSE_TEST_RECORD")
-    if rec_dir:  # the fit behind bench full_sweep.tolerance_at_t_final (profiles/r04/dense_growth_n14.json)
+    if rec_dir:  # the fit behind bench full_sweep.tolerance_at_t_final (profiles/r05/dense_growth_n14.json)
         with open(os.path.join(rec_dir, "dense_growth_n14.json"), "w") as f:
             json.dump({"intervals": K, "t": tk.tolist(), "max_abs_diff": err.tolist(), "hnorm_bound": hnorm,
                        "rate_ls_per_s": slope_ls, "rate_envelope_per_s": slope_env,
-                       "stated_at_30s": 1e-10 + 1.5 * eps * hnorm * 30.0}, f, indent=1)
-    assert np.all(err <= bound), (err, bound)
-    assert slope_env * 30.0 <= 1e-10 + 1.5 * eps * hnorm * 30.0
+                       "eps_hnorm_per_s": float(np.finfo(float).eps * hnorm)}, f, indent=1)
+    eps = np.finfo(float).eps
+    assert np.all(err <= 1e-10 + 1.5 * eps * hnorm * tk), err
+
+
+def test_dense_30s_n14_two_eigensolvers_agree(engine):
+    """The whole 30 s grid at N = 14 (3 variants at 150 kHz, the stiffest point) through the
+    two-stage eigensolver (eig_impl 1, the default) and through rocSOLVER dsyevd (eig_impl 0).
+    Each carries its own eigenvector rounding; with refined eigenvalues neither error grows with
+    t, so the two traces agree at t = 30 s as closely as at the first outputs (north_star 1e-8)."""
+    t_ref = np.linspace(0.0, 30.0, 20000)
+    params = [sweep_point_params(13, 150e3, v, 30.0, 20000) for v in VARIANTS]
+    ts, st, _ = _evolve(engine, params, t_ref, 2, eig_impl=1)
+    ev, st0, _ = _evolve(engine, params, t_ref, 2, eig_impl=0)
+    assert st["dense_problems"] == 3 and st0["dense_problems"] == 3
+    d = np.max(np.abs(ts[:, :6] - ev[:, :6]), axis=(0, 1))
+    early, late = float(d[:100].max()), float(d[-100:].max())
+    print(f"N=14 30 s grid, two-stage vs dsyevd: max {d.max():.2e} (first 100 outputs {early:.2e}, "
+          f"last 100 {late:.2e})")
+    rec_dir = os.environ.get("DSE_TEST_RECORD")
+    if rec_dir:
+        with open(os.path.join(rec_dir, "dense_solvers_n14_30s.json"), "w") as f:
+            json.dump({"max": float(d.max()), "first_100": early, "last_100": late,
+                       "every_1000": d[::1000].tolist()}, f, indent=1)
+    assert d.max() <= 1e-9   # measured 4.6e-11, flat in t (first and last 100 outputs 3.5e-11)
 
 
 def test_half_eigensolver_config2_matches_exact_and_dsyevd(engine, golden):
@@ -235,3 +256,30 @@ def test_two_stage_eigensolver_small_registers_match_dsyevd(engine, n_sea):
     tol = 1e-11 + 1e-8 * t
     assert np.all(np.abs(ts - ev) <= tol), np.max(np.abs(ts - ev) - tol)
     assert np.max(np.abs(s_ts[0] - s_ev[0])) < 1e-8
+
+
+def test_two_stage_poll_give_up_falls_back_to_dsyevd(engine):
+    """The two-stage eigensolver's cross-workgroup polls are bounded (option eig_spin_limit): a
+    give-up sets the solve's device error word, the launch drains, and the dense engine re-solves
+    that register with rocSOLVER dsyevd (stats eig_fallbacks).  -1 forces the give-up on every
+    solve; the result is then dsyevd's (1e-11)."""
+    t = np.linspace(0.0, 2e-3, 201)
+    p = sweep_point_params(11, 50000.0, "center_on", 2e-3, 201)   # 2^12: two-stage under eig_impl 3
+    ok, st_ok, _ = _evolve(engine, [p], t, 2, eig_impl=3)
+    assert st_ok["dense_problems"] == 1 and st_ok["eig_fallbacks"] == 0
+    engine.set_option("eig_spin_limit", -1)
+    try:
+        fb, st_fb, s_fb = _evolve(engine, [p], t, 2, eig_impl=3)
+        tiny, st_tiny, _ = _evolve(engine, [p], t, 2, eig_impl=3)   # still -1: repeatable
+    finally:
+        engine.set_option("eig_spin_limit", 1 << 22)
+    ev, st_ev, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st_fb["dense_problems"] == 1 and st_fb["eig_fallbacks"] == 1
+    assert st_tiny["eig_fallbacks"] == 1
+    assert st_ev["eig_fallbacks"] == 0
+    assert np.all(np.isfinite(fb))
+    np.testing.assert_allclose(fb, ev, rtol=0, atol=1e-11)
+    np.testing.assert_allclose(ok, ev, rtol=0, atol=1e-11)
+    assert np.max(np.abs(s_fb[0] - s_ev[0])) < 1e-11
+    again, st_again, _ = _evolve(engine, [p], t, 2, eig_impl=3)   # the context is fine afterwards
+    assert st_again["eig_fallbacks"] == 0 and np.array_equal(again, ok)

@@ -7,10 +7,11 @@ n_sea = 6 (its __main__ run, :1240), pinned by 40-digit eigendecompositions
 The two fixtures themselves differ by <= 1.3e-9 at 30 s: the rounding of the reference's diagonal
 sums, i.e. how well an fp64 H determines <O>(30 s) at all.
 
-* The dense engine (the engine the cost model picks for this grid) is held to the fp64 floor of an
-  eigendecomposition, |d<O>(t)| <= 1e-10 + 1.5 eps ||H|| t (2.1e-8 at 30 s), at every pinned output;
-  with and without its refinement (option dense_refine: double-double Rayleigh-quotient
-  eigenvalues with the exact diagonal, phases reduced modulo 2 pi in double-double), both reported.
+* The dense engine (the engine the cost model picks for this grid) is held to north_star's 1e-8 at
+  every pinned output, 30 s included, against both fixtures, with its refinement (option
+  dense_refine: double-double Rayleigh-quotient eigenvalues with the exact diagonal, phases reduced
+  modulo 2 pi in double-double).  Without the refinement (reported, not asserted) the eigenvalue
+  rounding grows like eps |lambda| t.
 * The small-register Chebyshev engine (k_small) on the grid's first 100 intervals (0.15 s).
 """
 import numpy as np
@@ -23,7 +24,7 @@ pytestmark = pytest.mark.gpu
 OBS = ("Ix_sea", "Iy_sea", "Iz_sea", "Iz_R", "Ix_R", "Iy_R")
 DELTAS = (0, 25000, 150000)
 T = np.linspace(0.0, 30.0, 20000)
-FLOOR_FACTOR = 1.5        # dense engine: |d<O>(t)| <= 1e-10 + 1.5 eps ||H|| t (the fp64 eigenvector floor)
+TOL_NORTH_STAR = 1e-8     # dense engine, every pinned output up to t = 30 s (BASELINE.json north_star)
 TOL_SMALL_PREFIX = 1e-10  # k_small over the first 0.15 s
 
 
@@ -68,19 +69,16 @@ def _err_t(g, obs, idx, src):
 
 
 def test_dense_engine_on_the_30s_grid_matches_high_precision(engine, golden):
-    """Held to the fp64 floor of an eigendecomposition: eigenvalues AND eigenvectors of a
-    backward-stable solver carry ~eps ||H|| relative errors (for a cluster of eigenvalues at gap
-    d the eigenvectors mix by ~eps ||H|| / d, which the phases turn into ~eps ||H|| t), so
-    |d<O>(t)| <= 1e-10 + FLOOR_FACTOR eps ||H|| t, with ||H|| the largest |lambda| of the fixture
-    (3.2e6 rad/s: 2.1e-8 at 30 s).  The refinement (double-double Rayleigh quotients, phases
-    reduced in double-double) removes the eigenvalue and phase-rounding parts; what remains is
-    the eigenvectors' share."""
+    """North_star's 1e-8 at every pinned output of the 30 s grid.  With double-double Rayleigh
+    quotients the eigenvalues carry ~eps^2 |H| errors and the output phases are reduced exactly,
+    so what grows with t is gone; the eigenvectors' own rounding (~eps) does not grow with t
+    (a rotation between eigenvectors at gap d turns into a phase error d t only for d t < 2, i.e.
+    for exactly degenerate levels, where it is harmless).  The unrefined run is reported."""
     g = golden("grid30_n7.npz")
     idx = g["t_index"]
     t = g["t"]
     assert np.array_equal(t, T[idx])
     hnorm = max(float(np.max(np.abs(g[f"{v}_{d}_lambda"]))) for v in VARIANTS for d in DELTAS)
-    bound = 1e-10 + FLOOR_FACTOR * np.finfo(float).eps * hnorm * t
     res = {}
     for refine in (0, 1):
         obs, st = _run(engine, T, dense_refine=refine)
@@ -89,11 +87,11 @@ def test_dense_engine_on_the_30s_grid_matches_high_precision(engine, golden):
         res[refine] = (_err_t(g, obs, idx, "tables"), _err_t(g, obs, idx, "ref"))
         et, er = res[refine]
         print(f"30 s grid, dense_refine={refine}: max |d<O>| vs tables-H {et.max():.2e} (t <= 1.5 s: "
-              f"{et[t <= 1.5].max():.2e}), vs reference-H {er.max():.2e}; max err / (eps ||H|| t) = "
-              f"{np.max(et / (np.finfo(float).eps * hnorm * t)):.2f}")
+              f"{et[t <= 1.5].max():.2e}, at 30 s {et[-1]:.2e}), vs reference-H {er.max():.2e}; "
+              f"max err / (eps ||H|| t) = {np.max(et / (np.finfo(float).eps * hnorm * t)):.3f}")
     et, er = res[1]
-    assert np.all(et <= bound), (et, bound)
-    assert np.all(er <= bound + 2e-9), (er, bound)   # + the two fixtures' own difference (<= 1.3e-9)
+    assert np.all(et <= TOL_NORTH_STAR), et
+    assert np.all(er <= TOL_NORTH_STAR), er   # includes the two fixtures' own difference (<= 1.3e-9)
 
 
 def test_small_register_engine_on_the_30s_grid_prefix(engine, golden):

@@ -115,3 +115,60 @@ def test_handoff_with_release_acquire_fences(engine):
         res[f] = obs
     np.testing.assert_allclose(res[1], res[0], rtol=0, atol=1e-13)
     engine.clear()
+
+
+def _run_states(engine, probs, t):
+    engine.clear()
+    for p in probs:
+        engine.add(p)
+    obs, st = engine.evolve(t)
+    states = [engine.state(i) for i in range(len(probs))]
+    return obs, st, states
+
+
+def test_handoff_fallback_keeps_dense_registers_state(engine):
+    """A context holding a dense-engine register beside a 2-tile register: after a hand-off timeout
+    the evolve re-runs the Chebyshev registers on the streaming kernels and keeps the dense
+    register's first-pass results -- its observables AND its final state (dse_get_state)."""
+    import dataclasses
+    dense_p = pb.build_problem(sweep_point_params(6, 75e3, "center_on", float(T[-1]), len(T)))
+    # a drive phase off pi/2 makes the 14-qubit register's drives complex: not dense-eligible
+    cheb_p = pb.build_problem(dataclasses.replace(sweep_point_params(13, 75e3, "shell_off", float(T[-1]), len(T)),
+                                                  phi_sea=0.3))
+    engine.set_option("dense", 2)
+    try:
+        ref, st, s_ref = _run_states(engine, [dense_p, cheb_p], T)
+        assert st["dense_problems"] == 1 and st["handoff_fallbacks"] == 0
+        engine.set_option("spin_limit", -1)
+        try:
+            got, st2, s_got = _run_states(engine, [dense_p, cheb_p], T)
+        finally:
+            engine.set_option("spin_limit", 1 << 22)
+    finally:
+        engine.set_option("dense", 1)
+        engine.clear()
+    assert st2["dense_problems"] == 1 and st2["handoff_fallbacks"] >= 1
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12)
+    assert np.array_equal(s_got[0], s_ref[0])            # the dense register's final state
+    np.testing.assert_allclose(s_got[1], s_ref[1], rtol=0, atol=1e-12)
+
+
+def test_span_handoff_failure_falls_back(engine):
+    """k_span with an explicit tile (span_tile = 11: 8 workgroups per 14-qubit register): every
+    partner wait failing (spin_limit = -1) re-runs the evolve on the streaming kernels with the
+    same results."""
+    probs = _two_tile_problems()
+    engine.set_option("span_tile", 11)
+    try:
+        ref, st, _ = _run_states(engine, probs, T)
+        assert st["span_problems"] == len(probs) and st["handoff_fallbacks"] == 0
+        engine.set_option("spin_limit", -1)
+        try:
+            got, st2, _ = _run_states(engine, probs, T)
+        finally:
+            engine.set_option("spin_limit", 1 << 22)
+    finally:
+        engine.set_option("span_tile", 0)
+        engine.clear()
+    assert st2["handoff_fallbacks"] >= 1
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12)

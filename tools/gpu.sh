@@ -4,7 +4,7 @@
 #   tools/gpu.sh <tag> <task>[:arg,arg...] [<task>...]
 #
 # Every task runs under its own time limit; the first failure ends the call (no GPU step after
-# a fault, an abort or a time limit).  Outputs land in gpurun_out/r04/<tag>/.
+# a fault, an abort or a time limit).  Outputs land in gpurun_out/r05/<tag>/.
 #   tests[:pytest-path-or-k]   pytest -m gpu (whole suite, a file, or "-k expr" as k=expr)
 #   smoke                      __graft_entry__.smoke()
 #   bench[:args]               python bench.py <args>  (args: comma-separated)
@@ -17,7 +17,7 @@
 #   py:<script>,<args...>      python -u <script> <args> > <tag>/<script-name>.out
 set -o pipefail
 TAG=${1:?tag}; shift
-OUT=gpurun_out/r04/$TAG
+OUT=gpurun_out/r05/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 LEGS="--no-cpu-baseline --no-large --no-full --no-config2 --no-refdefault"

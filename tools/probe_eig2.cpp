@@ -1,5 +1,5 @@
 // Probe (round 4): the two-stage eigensolver (dse_eig2.hip) against rocSOLVER dsyevd.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iquantumsimulations_amd/csrc tools/probe_eig2.cpp \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DDSE_EIG2_VARIANTS -Iquantumsimulations_amd/csrc tools/probe_eig2.cpp \
 //         quantumsimulations_amd/csrc/dse_eig2.hip quantumsimulations_amd/csrc/dse_sytrd.hip \
 //         -lrocsolver -lrocblas -o tools/bin/probe_eig2
 //   probe_eig2 <dim> [random]
@@ -123,7 +123,7 @@ int main(int argc, char** argv) {
     int rc1 = dse::sy2sb_lower(h, st, n, A, n, work);
     CK(hipStreamSynchronize(st));
     t[1] = now_ms();
-    int rc2 = dse::sb2st_lower(st, n, A, n, lam, e, work, n_cu, dbg);
+    int rc2 = dse::sb2st_lower(st, n, A, n, lam, e, work, n_cu, dse::kEig2DefaultSpin, dbg);
     CK(hipStreamSynchronize(st));
     t[2] = now_ms();
     rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, n, info);
