@@ -21,9 +21,10 @@ Extra fields of the JSON line:
                  rate alongside; "traffic" = the counter-measured bytes per launch
                  (profiles/<round>/bench_pmc_traffic.json)
   full_sweep     the reference's own grid (t_final 30 s, 20000 outputs, sweep_sea_detuning.py:
-                 1223-1224) on the same 64 x 3 evolutions: the first 16 output intervals timed 3
-                 times (spread reported), extrapolated to all 19999 -> points/hour and ms per ODE
-                 step: BASELINE's "(full sweep)" figure (`value` is the 1 ms head-to-head grid)
+                 1223-1224) on the same 64 x 3 evolutions: BASELINE's "(full sweep)" figure (`value`
+                 is the 1 ms head-to-head grid), by the fastest engine whose stated accuracy at
+                 t = 30 s meets north_star's 1e-8 -- the dense eigen-propagator timed on the whole
+                 sweep; the Chebyshev kernels (16 intervals x 3, extrapolated) beside it
   cpu_baseline   rank 0, N = 1 only: the QuTiP-5 sesolve equivalent (oracle/cpu_bench.py) on
                  the host cores, 1 core, this job's CPU share and a node-wide estimate, run
                  before the GPU is touched
@@ -47,6 +48,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -197,14 +199,28 @@ def large_register(device: int, n_sea: int = 29):
     s8d = 80.0 * (1 << n) / (per_term_ms * 1e-3) / 1e9
     fpa = flops_per_amp(prob)
     fl = fpa * (1 << n)
-    traffic = None  # HBM-side bytes per H application (MODE_GEN passes) from the counter passes
+    # HBM-side bytes per H application: the MODE_GEN (2) launches of the five passes in the counter
+    # record (template keys k_wht<13, pass, 2[, vectors]>, one launch per pass and H application);
+    # a missing record or pass is an explicit error, never a silent null
+    traffic, traffic_error = None, None
     try:
         with open(WHT_PMC_N30) as f:
             k = json.load(f)["kernels"]
-        if n == 30:
-            traffic = sum(k[f"k_wht<13, {ps}, 2>"]["traffic_bytes_per_launch"] for ps in range(5))
-    except (OSError, KeyError, ValueError):
-        pass
+        if n != 30:
+            traffic_error = f"counter record is for N = 30, this register is N = {n}"
+        else:
+            per_pass = {}
+            for name, rec in k.items():
+                m = re.fullmatch(r"k_wht<13, (\d), 2(?:, \d+)?>", name)
+                if m:
+                    per_pass[int(m.group(1))] = per_pass.get(int(m.group(1)), 0.0) + rec["traffic_bytes_per_launch"]
+            missing = [ps for ps in range(5) if ps not in per_pass]
+            if missing:
+                traffic_error = f"passes {missing} missing from {os.path.relpath(WHT_PMC_N30, ROOT)}"
+            else:
+                traffic = sum(per_pass.values())
+    except (OSError, KeyError, ValueError) as exc:
+        traffic_error = f"counter record unreadable: {exc!r}"
     check = {"max_norm_error": float(np.max(np.abs(obs[0, 6] - 1.0))),
              "energy_rel_error": abs(energy - e0) / abs(e0), "energy": energy, "energy_t0": e0,
              "final_norm2": norm2}
@@ -227,126 +243,143 @@ def large_register(device: int, n_sea: int = 29):
                      "passes_hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_amp_per_h": bpa},
                      "traffic": traffic, "traffic_per_amp": traffic / (1 << n) if traffic else None,
-                     "traffic_source": os.path.relpath(WHT_PMC_N30, ROOT) if traffic else None},
+                     "traffic_source": os.path.relpath(WHT_PMC_N30, ROOT) if traffic else None,
+                     **({"traffic_error": traffic_error} if traffic_error else {})},
         "check": check,
     }
 
 
-def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, dist=None,
-               dense_points=(0.0, 150e3)):
-    """The reference's grid (sweep_sea_detuning.py:1223-1224: t_final 30 s, 20000 outputs ->
-    dt = 1.5 ms, alpha dt ~ 3e3..1e4: one output per launch, ~1e4 Chebyshev terms each) on the
-    bench's evolutions: one interval untimed (coefficients, warm-up), then `repeats` timed runs of
-    the first `intervals` output intervals (barrier + device sync around each, max over ranks),
-    extrapolated linearly to all 19999 intervals (every interval has the same length, so the same
-    work); the spread over the repeats is reported."""
+def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, dist=None):
+    """BASELINE's "(full sweep)" figure: the reference's grid (sweep_sea_detuning.py:1223-1224:
+    t_final 30 s, 20000 outputs) on the bench's own evolutions (this rank's share of the 64-point
+    sweep, 3 variants per point).  Two engines, each with its stated accuracy at t = 30 s
+    (tolerance_at_t_final); the quoted one is the fastest whose stated accuracy meets north_star's
+    1e-8, the other is reported beside it.
+      dense      the dense eigen-propagator (libdse's cost model picks it for this grid) on the
+                 WHOLE sweep: one evolve of all the rank's registers over all 20000 outputs, timed
+                 whole (barrier + device sync around, max over ranks) -- measured, not extrapolated;
+      chebyshev  the Chebyshev kernels on the first `intervals` output intervals (`repeats` timed
+                 runs, spread reported), extrapolated linearly to all 19999 (every interval has the
+                 same length, so the same work; dt = 1.5 ms: alpha dt ~ 3e3..1e4 terms each)."""
     t_ref = np.linspace(0.0, 30.0, 20000)
-    eng.evolve(t_ref[:2])
-    stats, per = [], []
-    for _ in range(max(1, repeats)):
-        dt = timed_steps(lambda: stats.append(eng.evolve(t_ref[:intervals + 1])[1]), 1, 0, sync, dist)
-        per.append(dt / intervals)
+    eng.set_option("dense", 0)
+    try:
+        eng.evolve(t_ref[:2])
+        stats, per = [], []
+        for _ in range(max(1, repeats)):
+            dt = timed_steps(lambda: stats.append(eng.evolve(t_ref[:intervals + 1])[1]), 1, 0, sync, dist)
+            per.append(dt / intervals)
+    finally:
+        eng.set_option("dense", 1)
     st = stats[-1]
     per_interval = float(np.mean(per))
-    full_s = per_interval * (len(t_ref) - 1)
+    cheb_s = per_interval * (len(t_ref) - 1)
     h_per_ev = st["h_applications"] / len(probs) / intervals     # H applications per evolution
     k_ms = st["step_kernel_ms"]
     gbs = 80.0 * st["timed_amp_terms"] / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     cheb = {
-        "grid": "t_final 30 s, 20000 outputs (sweep_sea_detuning.py:1223-1224)",
+        "engine": "chebyshev",
         "intervals_timed": intervals, "repeats": len(per), "s_per_interval": per_interval,
         "s_per_interval_min": float(np.min(per)), "s_per_interval_max": float(np.max(per)),
         "spread_rel": float((np.max(per) - np.min(per)) / per_interval),
-        "full_sweep_s_extrapolated": full_s,
-        "value": n_points * 3600.0 / full_s, "unit": "detuning-points/hour (extrapolated)",
+        "full_sweep_s": cheb_s, "timing": "extrapolated from the first intervals",
+        "value": n_points * 3600.0 / cheb_s, "unit": "detuning-points/hour",
         "ms_per_ode_step": per_interval * 1e3 / h_per_ev,
         "h_applications_per_evolution_per_interval": h_per_ev,
         "max_degree": st["max_degree"], "outputs_per_launch": st["outputs_per_launch"],
         "engine_mode": {1: "persistent", 2: "walsh-hadamard"}.get(st["mode"], "streaming"),
         "kernel_gbs_80B_per_amp_term": gbs,
         "kernel_frac_hbm": gbs / HBM_PEAK_GBS if gbs else None,
+        "tolerance_at_t_final": tolerance_at_t_final(probs, False, t_ref[-1], len(t_ref) - 1),
     }
-    out = {"grid": cheb["grid"], "chebyshev": cheb}
-    dense = None
-    if dense_points:
-        try:
-            dense = full_sweep_dense(eng.device, dense_points, sync, dist)
-        except Exception as exc:  # report, never hide
-            dense = {"error": repr(exc)}
-        out["dense"] = dense
-    best = cheb
-    if dense and dense.get("full_sweep_s_extrapolated") and dense["full_sweep_s_extrapolated"] < full_s:
-        best = dense
-    out["tolerance_at_t_final"] = tolerance_at_t_final(probs, best is dense, t_ref[-1], len(t_ref) - 1)
-    out.update({
-        "engine": "dense eigen-propagator" if best is dense else "chebyshev",
-        "full_sweep_s_extrapolated": best["full_sweep_s_extrapolated"],
-        "value": n_points * 3600.0 / best["full_sweep_s_extrapolated"],
-        "unit": "detuning-points/hour (extrapolated)",
-        "note": "BASELINE's '(full sweep)' figure: the reference grid on the bench's 64 x 3 evolutions, by "
-                "the engine libdse's cost model picks for that grid (option dense = 1: the dense "
-                "eigen-propagator, whose cost per evolution does not depend on the detuning, timed whole "
-                "on sample points and scaled to 64; the Chebyshev engines timed on 16-interval runs and "
-                "scaled to 19999 intervals); headline `value` is the 1 ms head-to-head grid; the "
-                "reference's own ZVODE trace of this grid takes ~430-1530 h per N=14 evolution on one "
-                "core (SURVEY.md §6)",
-    })
+    dense = {"engine": "dense eigen-propagator"}
+    try:
+        dstats = []
+        dt = timed_steps(lambda: dstats.append(eng.evolve(t_ref)[1]), 1, 0, sync, dist)
+        dst = dstats[-1]
+        dense.update({
+            "full_sweep_s": dt, "timing": "the whole sweep timed (one evolve of every register over all 20000 outputs)",
+            "value": n_points * 3600.0 / dt, "unit": "detuning-points/hour",
+            "s_per_point": dt / (len(probs) / 3), "dense_problems": dst["dense_problems"],
+            "eig_fallbacks": dst.get("eig_fallbacks"),
+            "dense_ms": dst["dense_ms"], "eig_ms": dst["dense_eig_ms"],
+            "tolerance_at_t_final": tolerance_at_t_final(probs, True, t_ref[-1], len(t_ref) - 1),
+        })
+        if dst["dense_problems"] != len(probs):
+            dense["error"] = f"{dst['dense_problems']} of {len(probs)} registers on the dense engine"
+    except Exception as exc:  # report, never hide
+        dense["error"] = repr(exc)
+    ok = [e for e in (dense, cheb) if "error" not in e and e.get("full_sweep_s")
+          and e["tolerance_at_t_final"]["value"] <= NORTH_STAR_TOL]
+    best = min(ok, key=lambda e: e["full_sweep_s"]) if ok else None
+    out = {"grid": "t_final 30 s, 20000 outputs (sweep_sea_detuning.py:1223-1224)", "north_star_tol": NORTH_STAR_TOL}
+    if best is None:
+        out["error"] = "no engine meets north_star's 1e-8 at t = 30 s"
+    else:
+        out.update({"engine": best["engine"], "full_sweep_s": best["full_sweep_s"], "timing": best["timing"],
+                    "value": best["value"], "unit": "detuning-points/hour",
+                    "tolerance_at_t_final": best["tolerance_at_t_final"]})
+    out["dense"], out["chebyshev"] = dense, cheb
+    out["note"] = ("BASELINE's '(full sweep)' figure: the reference grid on the bench's 64 x 3 evolutions by "
+                   "the fastest engine whose stated accuracy at t = 30 s meets north_star's 1e-8; headline "
+                   "`value` is the 1 ms head-to-head grid; the reference's own ZVODE trace of this grid "
+                   "takes ~430-1530 h per N=14 evolution on one core (SURVEY.md §6)")
     return out
 
 
-DENSE_GROWTH_N14 = os.path.join(ROOT, "profiles", "r04", "dense_growth_n14.json")
+NORTH_STAR_TOL = 1e-8
+# -m gpu records of the accuracy on the 30 s grid (tools/gpu.sh tests with DSE_TEST_RECORD), newest first
+DENSE_SOLVERS_N14 = os.path.join(ROOT, "profiles", "r05", "dense_solvers_n14_30s.json")
+GRID30_N7 = os.path.join(ROOT, "profiles", "r05", "grid30_n7_errors.json")
+CHEB_DRIFT_N14 = os.path.join(ROOT, "profiles", "r05", "dense_growth_n14.json")
+DENSE_TOL_ASSERTED = 1e-9   # tests/test_gpu_dense.py::test_dense_30s_n14_two_eigensolvers_agree
+
+
+def _record(path):
+    try:
+        with open(path) as f:
+            return json.load(f), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        return None, None
 
 
 def tolerance_at_t_final(probs, dense: bool, t_final: float, intervals: int) -> dict:
-    """The stated accuracy of <O>(t_final) on the reference grid.  Dense engine: the fp64
-    eigenvector floor |d<O>(t)| <= 1e-10 + 1.5 eps ||H|| t, pinned at N = 7 against the mpmath
-    fixture (tests/test_gpu_grid30.py) and at N = 14 against the Chebyshev kernels over the grid's
-    first 100 intervals (tests/test_gpu_dense.py; the fitted growth rate, when its record is in
-    profiles/r04, extrapolated to t_final).  ||H|| <= the largest Gershgorin bound of the bench's
-    registers.  Chebyshev: the truncation tolerance 1e-14 per interval, summed."""
+    """The stated accuracy of <O>(t_final) on the reference grid.
+    Dense engine: double-double Rayleigh-quotient eigenvalues and phases, so nothing grows with t;
+    the -m gpu suite asserts 1e-8 at every pinned output to 30 s against the 40-digit N = 7
+    fixture (tests/test_gpu_grid30.py) and 1e-9 between two independent eigensolvers over the
+    whole 30 s grid at N = 14 (tests/test_gpu_dense.py); the stated value is that 1e-9, the
+    measured figures beside it.
+    Chebyshev: the truncation 1e-14 per interval, summed, plus its fp64 drift -- ~1e4 fp64 H
+    applications per interval are the exact evolution of an H perturbed by ~eps ||H||, so its trace
+    drifts linearly in t; the rate measured against the dense engine over the grid's first 0.15 s
+    at N = 14 (its envelope) is extrapolated to t_final."""
     from quantumsimulations_amd import problem as pb
     eps = float(np.finfo(float).eps)
     hnorm = max(max(abs(a) for a in pb.spectral_bounds(p)) for p in probs)
     out = {"engine": "dense" if dense else "chebyshev", "t_final_s": float(t_final), "hnorm_bound": hnorm,
-           "north_star": 1e-8}
+           "north_star": NORTH_STAR_TOL}
     if dense:
-        out.update({"value": 1e-10 + 1.5 * eps * hnorm * t_final, "formula": "1e-10 + 1.5 eps ||H|| t"})
-        if os.path.exists(DENSE_GROWTH_N14):
-            with open(DENSE_GROWTH_N14) as f:
-                g = json.load(f)
-            out["measured_n14"] = {"rate_per_s": g["rate_envelope_per_s"], "at_t_final": g["rate_envelope_per_s"] * t_final,
-                                   "source": os.path.relpath(DENSE_GROWTH_N14, ROOT)}
+        out.update({"value": DENSE_TOL_ASSERTED,
+                    "basis": "asserted in -m gpu: N=14 two-stage vs dsyevd over the whole 30 s grid <= 1e-9; "
+                             "N=7 vs the 40-digit fixture <= 1e-8 at every pinned output"})
+        rec, src = _record(DENSE_SOLVERS_N14)
+        if rec:
+            out["measured_n14_two_solvers"] = {"max": rec["max"], "first_100": rec["first_100"],
+                                               "last_100": rec["last_100"], "source": src}
+        rec, src = _record(GRID30_N7)
+        if rec:
+            out["measured_n7_vs_40_digits"] = {"max": rec["max_vs_tables"], "at_30s": rec["at_30s_vs_tables"],
+                                               "source": src}
     else:
-        out.update({"value": 1e-14 * intervals, "formula": "1e-14 per interval x intervals"})
+        drift = None
+        rec, src = _record(CHEB_DRIFT_N14)
+        if rec:
+            drift = rec["rate_envelope_per_s"] * t_final
+            out["measured_drift_n14"] = {"rate_per_s": rec["rate_envelope_per_s"], "source": src}
+        out.update({"value": 1e-14 * intervals + (drift if drift is not None else 1.5 * eps * hnorm * t_final),
+                    "formula": "1e-14 per interval x intervals + fp64 drift rate x t_final"})
     return out
-
-
-def full_sweep_dense(device: int, dets, sync, dist=None):
-    """The dense eigen-propagator on the WHOLE reference grid (20000 outputs) for the 3 variants of
-    the sample detunings, one evolve per detuning (timed whole, barrier + sync around): its work per
-    evolution is one eigendecomposition + the output GEMMs, independent of the detuning, so the
-    sweep's cost = 64 x the mean per-point time (the sample's spread reported)."""
-    from quantumsimulations_amd import problem as pb
-    from quantumsimulations_amd.engine import Engine
-    from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params
-    t_ref = np.linspace(0.0, 30.0, 20000)
-    per_point, stats = [], []
-    with Engine(device) as eng:
-        for d in dets:
-            eng.clear()
-            for v in VARIANTS:
-                eng.add(pb.build_problem(sweep_point_params(N_SEA, float(d), v, 30.0, 20000)))
-            dt = timed_steps(lambda: stats.append(eng.evolve(t_ref)[1]), 1, 0, sync, dist)
-            per_point.append(dt)
-    st = stats[-1]
-    mean = float(np.mean(per_point))
-    return {
-        "sample_detunings_hz": [float(d) for d in dets], "s_per_point": per_point,
-        "s_per_point_mean": mean, "dense_problems": st["dense_problems"],
-        "eig_ms_last_point": st["dense_eig_ms"], "dense_ms_last_point": st["dense_ms"],
-        "full_sweep_s_extrapolated": mean * N_DET,
-        "value": N_DET * 3600.0 / (mean * N_DET),
-    }
 
 
 def matrix_kernels(st) -> dict:
@@ -531,6 +564,34 @@ def timed_steps(step, steps: int, warmup: int, sync, dist=None) -> float:
     return dt
 
 
+class Heartbeat:
+    """A progress line on stderr every `every` seconds while the bench runs (a long leg -- the whole
+    30 s-grid sweep on the dense engine is minutes of device work in one call -- is not a hang)."""
+
+    def __init__(self, every: float = 45.0):
+        import threading
+        self.phase, self.t0 = "start", time.time()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, args=(every,), daemon=True)
+        self._th.start()
+
+    def _run(self, every):
+        while not self._stop.wait(every):
+            print(f"[bench] {self.phase}: {time.time() - self.t0:.0f} s", file=sys.stderr, flush=True)
+
+    def stop(self):
+        self._stop.set()
+
+
+HEARTBEAT = None
+
+
+def phase(name: str) -> None:
+    if HEARTBEAT is not None:
+        HEARTBEAT.phase = name
+    print(f"[bench] {name}", file=sys.stderr, flush=True)
+
+
 def note(msg: str) -> None:
     """Progress on stderr (the JSON line is the only stdout)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -581,13 +642,16 @@ def partitioned_leg(rank: int, world: int, local: int, dist, timeout: float, cmd
 
 
 def main():
+    global HEARTBEAT
     args = parse()
+    HEARTBEAT = Heartbeat()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:  # before any GPU work: the CPU leg forks worker processes
+            phase("cpu_baseline")
             cpu = cpu_baseline(args.cpu_fraction, args.cpu_cores)
         except Exception as exc:  # report, never hide
             cpu = {"value": None, "error": repr(exc)}
@@ -636,6 +700,7 @@ def main():
             warm[0] -= 1
         else:
             stats.append(st)
+    phase("sweep (timed steps)")
     dt = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, dist)
 
     if world > 1:
@@ -757,31 +822,36 @@ def main():
         "roofline": roof,
     }
     if not args.no_full:
+        phase("full_sweep (30 s grid)")
         try:
-            line["full_sweep"] = full_sweep(eng, probs, args.n_det if args.scaling == "strong" else len(my_det) * world, args.full_intervals,
-                                            args.full_repeats, torch.cuda.synchronize, dist)
+            line["full_sweep"] = full_sweep(eng, probs, len(my_det) * world if args.scaling == "weak" else args.n_det,
+                                            args.full_intervals, args.full_repeats, torch.cuda.synchronize, dist)
         except Exception as exc:  # report, never hide
             line["full_sweep"] = {"error": repr(exc)}
     if cpu is not None:
         line["cpu_baseline"] = cpu
     if rank == 0 and world == 1 and not args.no_shard8:
         try:
+            phase("strong_shard_8gpu")
             line["strong_shard_8gpu"] = strong_shard_leg(eng, args.n_sea, args.n_det)
         except Exception as exc:  # report, never hide
             line["strong_shard_8gpu"] = {"error": repr(exc)}
     eng.close()
     if rank == 0 and world == 1 and not args.no_config2:
         try:
+            phase("config2")
             line["config2"] = config2_leg(local)
         except Exception as exc:  # report, never hide
             line["config2"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_refdefault:
         try:
+            phase("reference_default")
             line["reference_default"] = reference_default_leg(local)
         except Exception as exc:  # report, never hide
             line["reference_default"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_large:
         try:
+            phase("large_register")
             line["large_register"] = large_register(local)
         except Exception as exc:  # report, never hide
             line["large_register"] = {"error": repr(exc)}
@@ -793,6 +863,7 @@ def main():
             rep = {"error": repr(exc)}
         if rank == 0:
             line["partitioned"] = rep
+    HEARTBEAT.stop()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -2077,9 +2077,10 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         half_min = SIZE_MAX;
       }
     }
-    // the workers take tasks largest first; a job whose last register is solved goes to the output
-    // queue, and this thread runs its output GEMMs (dense_stream) while the other jobs' solves go on
-    // (a round's 2^14 registers' outputs under its 2^13 solve)
+    // the workers take tasks largest first; every solved register (a batched task: its whole job)
+    // goes to the output queue at once, and this thread runs its output GEMMs (dense_stream) while
+    // the other registers' solves go on (round 4 queued a job only when all its registers were
+    // solved, so a round's 2^14 outputs waited for its last 2^14 solve)
     std::atomic<size_t> next{0};
     std::atomic<bool> abort_all{false};
     std::vector<rocblas_status> wst(K, rocblas_status_success);
@@ -2087,9 +2088,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     std::vector<hipError_t> werr(K, hipSuccess);
     std::mutex qm;
     std::condition_variable qcv;
-    std::deque<DenseJob*> ready;
-    std::map<DenseJob*, int> pending;
-    for (const Task& T : tasks) pending[T.j] += 1;
+    std::deque<Task> ready;
     int workers_left = K;
     auto e1 = e0;
     auto worker = [&](int w) {
@@ -2134,44 +2133,47 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           break;
         }
         std::lock_guard<std::mutex> lk(qm);
-        if (--pending[&J] == 0) {
-          ready.push_back(&J);
-          qcv.notify_one();
-        }
+        ready.push_back(T);
+        qcv.notify_one();
       }
       std::lock_guard<std::mutex> lk(qm);
       if (--workers_left == 0) e1 = std::chrono::steady_clock::now();
       qcv.notify_one();
     };
-    auto outputs = [&](DenseJob& J) -> int {
-      const int cnt = J.cnt, TB = J.TB;
+    auto outputs = [&](const Task& T) -> int {  // registers [i0, i0 + cnt) of job T.j
+      DenseJob& J = *T.j;
+      const int i0 = T.i >= 0 ? T.i : 0, cnt = T.i >= 0 ? 1 : J.cnt, TB = J.TB;
       const size_t dim = J.dim, pstride = J.pstride;
+      const DenseProb* desc = J.d_desc + i0;
+      double* const V = J.V + dim * dim * i0;
+      double* const Pm = J.Pm + pstride * i0;
+      double* const Psi = J.Psi + pstride * i0;
       std::vector<rocblas_int> hinfo(cnt);
-      HIPC(hipMemcpyAsync(hinfo.data(), J.info, cnt * sizeof(rocblas_int), hipMemcpyDeviceToHost, st));
+      HIPC(hipMemcpyAsync(hinfo.data(), J.info + i0, cnt * sizeof(rocblas_int), hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
       for (int i = 0; i < cnt; ++i)
         if (hinfo[i] != 0)
           return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: eigensolver did not converge (info " +
                                                     std::to_string(hinfo[i]) + ")");
       const double one = 1.0, zero = 0.0;
-      if (ctx->dense_refine) HIPC(launch_dense_rq(J.d_desc, cnt, (int)dim, st));
+      if (ctx->dense_refine) HIPC(launch_dense_rq(desc, cnt, (int)dim, st));
       for (int tb0 = 0; tb0 < n_t; tb0 += TB) {
         const int tb = std::min(TB, n_t - tb0);
-        HIPC(launch_dense_phase(J.d_desc, cnt, (int)dim, d_tau + tb0, tb, J.Pm, pstride, st));
+        HIPC(launch_dense_phase(desc, cnt, (int)dim, d_tau + tb0, tb, Pm, pstride, st));
         const rocblas_status rs = rocblas_dgemm_strided_batched(
             ctx->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)dim, 2 * tb, (rocblas_int)dim, &one,
-            J.V, (rocblas_int)dim, (rocblas_stride)(dim * dim), J.Pm, (rocblas_int)dim, (rocblas_stride)pstride, &zero,
-            J.Psi, (rocblas_int)dim, (rocblas_stride)pstride, cnt);
+            V, (rocblas_int)dim, (rocblas_stride)(dim * dim), Pm, (rocblas_int)dim, (rocblas_stride)pstride, &zero,
+            Psi, (rocblas_int)dim, (rocblas_stride)pstride, cnt);
         if (rs != rocblas_status_success)
           return fail(ctx, DSE_ERR_HIP, "rocblas dgemm failed (status " + std::to_string((int)rs) + ")");
-        HIPC(launch_dense_obs(J.d_desc, cnt, (int)dim, J.Psi, pstride, tb, tb0, st));
-        if (tb0 + tb == n_t) HIPC(launch_dense_final(J.d_desc, cnt, (int)dim, J.Psi, pstride, tb, tau[n_t - 1], st));
+        HIPC(launch_dense_obs(desc, cnt, (int)dim, Psi, pstride, tb, tb0, st));
+        if (tb0 + tb == n_t) HIPC(launch_dense_final(desc, cnt, (int)dim, Psi, pstride, tb, tau[n_t - 1], st));
       }
       std::vector<double> h((size_t)n_t * 8 * cnt);
-      HIPC(hipMemcpyAsync(h.data(), J.obs, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPC(hipMemcpyAsync(h.data(), J.obs + (size_t)n_t * 8 * i0, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
       for (int i = 0; i < cnt; ++i) {
-        const int pi = J.list[i];
+        const int pi = J.list[i0 + i];
         for (int ti = 0; ti < n_t; ++ti)
           finish_obs(ctx->probs[pi], h.data() + ((size_t)i * n_t + ti) * 8,
                      obs_out + (size_t)pi * DSE_N_OBS * n_t + ti, (size_t)n_t);
@@ -2182,16 +2184,16 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     for (int w = 0; w < K; ++w) th.emplace_back(worker, w);
     int orc = DSE_OK;
     size_t done = 0;
-    while (done < jobs.size()) {
-      DenseJob* J = nullptr;
+    while (done < tasks.size()) {
+      Task T{nullptr, 0};
       {
         std::unique_lock<std::mutex> lk(qm);
         qcv.wait(lk, [&] { return !ready.empty() || workers_left == 0; });
         if (ready.empty()) break;  // the workers stopped early: an error below
-        J = ready.front();
+        T = ready.front();
         ready.pop_front();
       }
-      orc = outputs(*J);
+      orc = outputs(T);
       if (orc != DSE_OK) {
         abort_all = true;
         break;
@@ -2208,7 +2210,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       if (wrc[w] != 0)
         return fail(ctx, DSE_ERR_HIP, "half-matrix eigensolver failed (step " + std::to_string(-wrc[w]) + ")");
     }
-    if (done < jobs.size()) return fail(ctx, DSE_ERR_HIP, "dense engine: eigensolver workers stopped early");
+    if (done < tasks.size()) return fail(ctx, DSE_ERR_HIP, "dense engine: eigensolver workers stopped early");
     eig_ms += std::chrono::duration<double, std::milli>(e1 - e0).count();
   }
   if (ms_all) *ms_all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();

@@ -14,6 +14,9 @@ sums, i.e. how well an fp64 H determines <O>(30 s) at all.
   rounding grows like eps |lambda| t.
 * The small-register Chebyshev engine (k_small) on the grid's first 100 intervals (0.15 s).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -90,6 +93,13 @@ def test_dense_engine_on_the_30s_grid_matches_high_precision(engine, golden):
               f"{et[t <= 1.5].max():.2e}, at 30 s {et[-1]:.2e}), vs reference-H {er.max():.2e}; "
               f"max err / (eps ||H|| t) = {np.max(et / (np.finfo(float).eps * hnorm * t)):.3f}")
     et, er = res[1]
+    rec_dir = os.environ.get("DSE_TEST_RECORD")
+    if rec_dir:  # bench full_sweep.tolerance_at_t_final (profiles/r05/grid30_n7_errors.json)
+        with open(os.path.join(rec_dir, "grid30_n7_errors.json"), "w") as f:
+            json.dump({"t": t.tolist(), "err_vs_tables": et.tolist(), "err_vs_reference": er.tolist(),
+                       "max_vs_tables": float(et.max()), "at_30s_vs_tables": float(et[-1]),
+                       "max_vs_reference": float(er.max()), "unrefined_max_vs_tables": float(res[0][0].max())},
+                      f, indent=1)
     assert np.all(et <= TOL_NORTH_STAR), et
     assert np.all(er <= TOL_NORTH_STAR), er   # includes the two fixtures' own difference (<= 1.3e-9)
 

@@ -3,7 +3,10 @@
 variants of one detuning on the reference's 30 s / 20 000-output grid, evolved once per settings
 string, wall time and the engine's eigensolver / dense times as one JSON line each.
 
-    python3 tools/probe_fullsweep.py eig_streams=2 eig_streams=3,eig_impl=1 ...
+    python3 tools/probe_fullsweep.py eig_streams=2 eig_streams=3,eig_impl=1 points=16 ...
+
+points=K (not an engine option): K detunings of linspace(0, 150 kHz, K) in one evolve (3K
+registers), as bench.py's full_sweep evolves the whole sweep.
 """
 import json
 import os
@@ -21,10 +24,12 @@ from quantumsimulations_amd.sweep import VARIANTS, sweep_point_params  # noqa: E
 
 def main():
     t_ref = np.linspace(0.0, 30.0, 20000)
-    probs = [pb.build_problem(sweep_point_params(13, 50e3, v, 30.0, 20000)) for v in VARIANTS]
     with Engine(0) as eng:
         for settings in sys.argv[1:] or [""]:
             opts = dict(kv.split("=") for kv in settings.split(",") if kv)
+            npts = int(opts.pop("points", 0))
+            dets = np.linspace(0.0, 150e3, npts) if npts else [50e3]
+            probs = [pb.build_problem(sweep_point_params(13, float(d), v, 30.0, 20000)) for d in dets for v in VARIANTS]
             for k, v in opts.items():
                 eng.set_option(k, float(v))
             eng.clear()
@@ -33,7 +38,8 @@ def main():
             t0 = time.perf_counter()
             _, st = eng.evolve(t_ref)
             wall = time.perf_counter() - t0
-            print(json.dumps({"settings": settings, "wall_s": wall, "dense_problems": st["dense_problems"],
+            print(json.dumps({"settings": settings, "wall_s": wall, "s_per_point": wall / len(dets),
+                              "dense_problems": st["dense_problems"],
                               "eig_ms": st["dense_eig_ms"], "dense_ms": st["dense_ms"]}), flush=True)
 
 
