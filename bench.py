@@ -87,6 +87,8 @@ def parse():
                     "or one stream each (0)")
     ap.add_argument("--real", type=int, default=int(os.environ.get("DSE_REAL", "0")),
                     help="real-component mode (dse_real.hip) for the 13/14-qubit registers (0: k_interval)")
+    ap.add_argument("--span-tile", type=int, default=int(os.environ.get("DSE_SPAN_TILE", "-1")),
+                    help="k_span tile bits for the sweep's registers (-1 auto: only when all tiles fit at once; 0 never)")
     ap.add_argument("--obs-overlap", type=int, default=int(os.environ.get("DSE_OBS_OVERLAP", "0")),
                     help="persistent mode: observables on a second stream per lane (1)")
     ap.add_argument("--n-sea", type=int, default=N_SEA)
@@ -686,6 +688,7 @@ def main():
     eng.set_option("mixed_launch", args.mixed_launch)
     eng.set_option("obs_overlap", args.obs_overlap)
     eng.set_option("real", args.real)
+    eng.set_option("span_tile", args.span_tile)
     if os.environ.get("DSE_CORESIDENT"):  # diagnostics: workgroups per 2-tile interval launch chunk
         eng.set_option("coresident", float(os.environ["DSE_CORESIDENT"]))
     for p in probs:

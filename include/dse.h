@@ -195,9 +195,16 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "real"         1: registers of 13 / 14 qubits whose drives are all imaginary
  *                         (the sweep's phase pi/2) run in the rotated frame, where H is real: two
  *                         real Chebyshev recurrences, one workgroup each holding the whole
- *                         register in LDS (k_real, dse_real.hip); 0 (default): the complex
- *                         kernels (k_real measured at the 2-tile k_interval's CU cost, slower on
- *                         the bench's mix of 13- and 14-qubit registers)
+ *                         register in LDS (k_real, dse_real.hip); 2: only the 2-tile (14-qubit)
+ *                         registers real, beside the 13-qubit ones on the 1-tile k_interval;
+ *                         0 (default): the complex kernels (k_real measured at the 2-tile
+ *                         k_interval's CU cost: slower on the bench's mix, 1 and 2 alike)
+ *          "spin_limit"   persistent kernels: polls of a partner workgroup's flag before a
+ *                         cross-tile hand-off is declared failed (default 2^22, ~0.3 s; the call
+ *                         then re-runs on the streaming kernels, stats handoff_fallbacks);
+ *                         -1: every hand-off fails at once (tests)
+ *          "ablate", "span_ablate", "real_ablate"  diagnostics builds only (-DDSE_DIAG): skip
+ *                         kernel sections for timing (results become wrong); DSE_ERR_ARG here
  *          "span_tile"    L > 0 (10 or 11): every register of n > L qubits runs over 2^(n - L)
  *                         cooperating workgroups, one per CU, with per-term cross-tile hand-offs
  *                         (k_span, dse_span.hip): a shorter chain per register for few registers

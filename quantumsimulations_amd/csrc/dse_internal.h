@@ -148,6 +148,14 @@ struct alignas(16) SpanTab {
   // [2] [3] pairs (j, register bit 0..3), [4 + q] thread pair q of the iteration (mask bits, g)
   double2 it[kSpanMaxIt];
 };
+// Per-context options of the persistent kernels' cross-workgroup hand-offs, passed with every launch
+// (kernel arguments: distinct contexts on one process stay independent)
+struct HandoffKnobs {
+  int spin_limit = 1 << 22;  // polls of a partner's flag before the hand-off is declared failed
+                             // (s_sleep 1 between polls, ~0.3 s); < 0: every wait fails at once
+                             // (tests: exercises the fallback to the streaming kernels)
+  int fences = 0;            // k_interval: 1 adds an agent release / acquire around each flag
+};
 struct SpanDesc {
   const SpanTab* tab;
   double2* slots;  // [2^s tiles][s + 1 operand kinds: u_0..u_{s-1}, raw][kXSlots][2^L]
@@ -156,9 +164,8 @@ struct SpanDesc {
 };
 hipError_t launch_span(int L, int RB, bool imag, const DevProb* probs, const SpanDesc* sdesc,
                        const int2* items, int n_items, int q, int set, int n_out, int* err,
-                       hipStream_t st);
+                       HandoffKnobs hk, hipStream_t st);
 bool span_supported(int L, int RB);
-hipError_t set_span_spin_limit(int limit);
 hipError_t set_span_ablate(int mask);
 hipError_t set_real_ablate(int mask);
 hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu);
@@ -233,10 +240,10 @@ __device__ __forceinline__ const double2* tile_ptr(const DevProb& P, int role, u
 
 hipError_t launch_step(int L, int mode, const DevProb* probs, const int2* items, int n_items,
                        int k, int q, int set, hipStream_t st);
+// diagnostics builds only (-DDSE_DIAG, e.g. DSE_EXTRA_FLAGS for a tools/ variant library): kernel
+// section ablation masks; the product library returns hipErrorNotSupported
 hipError_t set_ablate(int mask);
 hipError_t set_ablate_interval(int mask);
-hipError_t set_spin_limit(int limit);
-hipError_t set_handoff_fences(int on);  // interval kernel: release/acquire around each hand-off
 bool interval_supported(int L);
 // resident workgroups of k_interval<L> per compute unit (occupancy query)
 hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu);
@@ -244,7 +251,8 @@ hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu);
 // colstride > 0: column mode (one-tile register, item.y = column, buffers offset by column *
 // colstride amplitudes): every column propagated over the interval of coefficient set `set`
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items, int q,
-                           int set, int n_out, int* flags, int* err, hipStream_t st, long colstride = 0);
+                           int set, int n_out, int* flags, int* err, HandoffKnobs hk, hipStream_t st,
+                           long colstride = 0);
 // zeroes the interval kernel's hand-off flags of the given items (before a 2-tile launch)
 hipError_t zero_flags(const int2* items, int n_items, int* flags, hipStream_t st);
 // psi(t0) of many registers in one launch: entry i zeroes ptr[0 .. n) and sets ptr[one_at] = 1

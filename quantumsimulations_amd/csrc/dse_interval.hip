@@ -46,30 +46,23 @@
 
 namespace dse {
 
-// Diagnostic ablation mask of k_interval (0 in production), see set_ablate.
+// Diagnostic ablation mask of k_interval (diagnostics builds, -DDSE_DIAG; 0 in libdse.so).
+#ifdef DSE_DIAG
 __device__ int g_dse_ablate_iv = 0;
-// Polls of a partner's flag before a hand-off is declared failed (s_sleep 1 between polls:
-// ~0.3 s at the default).  Diagnostics: a negative value fails every hand-off at its first wait,
-// which exercises the runtime's fallback to the streaming kernels.
-__device__ int g_dse_spin_limit = 1 << 22;
-// Hand-off protocol: 0 (default) the sc1 form -- sc1 payload stores and loads, per-wave
-// s_waitcnt vmcnt(0) + barrier before an sc1 flag store, sc1 poll (MI355X_MICROARCH.md, Valid
-// forms, table row 1); 1 adds an agent-scope release in front of every flag store and an
-// agent-scope acquire behind every poll (the placement-independent Guideline 16 recipe): -2.8%
-// points/h on the bench (profiles/r02/ab/handoff_fences.jsonl).
-__device__ int g_dse_handoff_fences = 0;
-
 hipError_t set_ablate_interval(int mask) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_ablate_iv), &mask, sizeof(int));
 }
-
-hipError_t set_spin_limit(int limit) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_spin_limit), &limit, sizeof(int));
-}
-
-hipError_t set_handoff_fences(int on) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_handoff_fences), &on, sizeof(int));
-}
+#else
+constexpr int g_dse_ablate_iv = 0;
+hipError_t set_ablate_interval(int mask) { return mask ? hipErrorNotSupported : hipSuccess; }
+#endif
+// Hand-off options (HandoffKnobs, per context, a kernel argument): spin_limit polls of a partner's
+// flag before a hand-off is declared failed (the runtime then re-runs on the streaming kernels);
+// fences 0 (default) the sc1 form -- sc1 payload stores and loads, per-wave s_waitcnt vmcnt(0) +
+// barrier before an sc1 flag store, sc1 poll (MI355X_MICROARCH.md, Valid forms, table row 1); 1
+// adds an agent-scope release in front of every flag store and an agent-scope acquire behind every
+// poll (the placement-independent Guideline 16 recipe): -2.8% points/h on the bench
+// (profiles/r02/ab/handoff_fences.jsonl).
 
 namespace {
 
@@ -144,7 +137,7 @@ struct IvShared {
 template <int L, bool IMAG>
 __global__ void __launch_bounds__(RB<L>::NT)
 k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, int q, int set,
-           int n_out, int* __restrict__ flags, int* __restrict__ err, long colstride) {
+           int n_out, int* __restrict__ flags, int* __restrict__ err, HandoffKnobs hk, long colstride) {
   constexpr int NT = RB<L>::NT, R = kRegAmps, TB = RB<L>::TB, NH = R / 2;
   // software-pipelined partner reads in the fused loop (the production IMAG build; the general
   // build keeps the plain order, which fits its larger drive arithmetic without spilling)
@@ -200,7 +193,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
   // diagnostics only (0 in production): 4 skip the register-bit terms, 64 skip the hand-off stores
   // and flag, 128 skip the partner wait and read, 256 skip the acc updates, 512 skip the tile terms
   const int ab = g_dse_ablate_iv;
-  const bool fences = g_dse_handoff_fences != 0;
+  const bool fences = hk.fences != 0;
 
   // ---- setup: tables, w_0 tile -> LDS, per-thread diagonal ----
   if (tid == 0) s_fail = 0;
@@ -536,7 +529,7 @@ k_interval(const DevProb* __restrict__ probs, const int2* __restrict__ items, in
       }
         if ((xgen || k > 1) && lane == 0 && !(ab & 64)) {  // w_0 of the partner is its psi tile
           int spins = 0;
-          const int limit = g_dse_spin_limit;
+          const int limit = hk.spin_limit;
           while (limit < 0 || __hip_atomic_load(flag_pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) {
             __builtin_amdgcn_s_sleep(1);
             // give up at the limit, or as soon as another pair has (its partner may never come)
@@ -681,17 +674,18 @@ hipError_t interval_occupancy(int L, bool imag, int* blocks_per_cu) {
 }
 
 hipError_t launch_interval(int L, bool imag, const DevProb* probs, const int2* items, int n_items,
-                           int q, int set, int n_out, int* flags, int* err, hipStream_t st, long colstride) {
+                           int q, int set, int n_out, int* flags, int* err, HandoffKnobs hk, hipStream_t st,
+                           long colstride) {
   if (n_items <= 0) return hipSuccess;
   switch (L) {
 #define X(l)                                                                                     \
   case l:                                                                                        \
     if (imag)                                                                                    \
       hipLaunchKernelGGL((k_interval<l, true>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs,  \
-                         items, q, set, n_out, flags, err, colstride);                                  \
+                         items, q, set, n_out, flags, err, hk, colstride);                        \
     else                                                                                         \
       hipLaunchKernelGGL((k_interval<l, false>), dim3(n_items), dim3(RB<l>::NT), 0, st, probs, \
-                         items, q, set, n_out, flags, err, colstride);                                  \
+                         items, q, set, n_out, flags, err, hk, colstride);                        \
     return hipGetLastError();
     X(10) X(11) X(12) X(13)
 #undef X

@@ -18,12 +18,17 @@
 
 namespace dse {
 
-// Diagnostic ablation mask (0 in production): sections of k_step_rb to skip, for timing only.
+// Diagnostic ablation mask (diagnostics builds, -DDSE_DIAG; 0 in libdse.so): sections of k_step_rb
+// to skip, for timing only.
 //   1 thread-bit sweeps   2 thread-thread pairs   4 cross-tile terms   8 epilogue global reads
 //   16 diagonal table read   32 tile load from global memory
+#ifdef DSE_DIAG
 __device__ int g_dse_ablate = 0;
-
 hipError_t set_ablate(int mask) { return hipMemcpyToSymbol(HIP_SYMBOL(g_dse_ablate), &mask, sizeof(int)); }
+#else
+constexpr int g_dse_ablate = 0;
+hipError_t set_ablate(int mask) { return mask ? hipErrorNotSupported : hipSuccess; }
+#endif
 
 namespace {
 

@@ -87,10 +87,14 @@ __device__ __forceinline__ void rd_pairs(uint32_t wbase, int tp, int hh, int pp0
   }
 }
 
-// diagnostics only (option real_ablate, separate instantiations; results become wrong): 1 phase 1,
-// 2 the sweeps' FMAs, 4 the thread pairs, 8 the propagator sums' global loads and stores, 16 the
-// w_k stores
+// diagnostics builds only (-DDSE_DIAG; option real_ablate, separate instantiations; results become
+// wrong): 1 phase 1, 2 the sweeps' FMAs, 4 the thread pairs, 8 the propagator sums' global loads and
+// stores, 16 the w_k stores
+#ifdef DSE_DIAG
 int g_real_ablate = 0;
+#else
+constexpr int g_real_ablate = 0;
+#endif
 
 template <int L, int ABL>
 __device__ __forceinline__ void real_body(RealShared& S, const DevProb& P, int comp, int set, int n_out) {
@@ -476,8 +480,12 @@ k_real_init(const DevProb* __restrict__ probs, const int2* __restrict__ items) {
 hipError_t set_real_ablate(int mask) {
   if (mask != 0 && mask != 1 && mask != 2 && mask != 4 && mask != 6 && mask != 8 && mask != 16)
     return hipErrorInvalidValue;
+#ifdef DSE_DIAG
   g_real_ablate = mask;
   return hipSuccess;
+#else
+  return mask ? hipErrorNotSupported : hipSuccess;
+#endif
 }
 
 hipError_t real_occupancy(int* blocks_per_cu) {
@@ -488,6 +496,7 @@ hipError_t launch_real(const DevProb* probs, const int2* items, int n_items, int
                        hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
   const dim3 g(n_items), b(kRealNT);
+#ifdef DSE_DIAG
   switch (g_real_ablate) {
     case 1: hipLaunchKernelGGL(k_real<1>, g, b, 0, st, probs, items, set, n_out); break;
     case 2: hipLaunchKernelGGL(k_real<2>, g, b, 0, st, probs, items, set, n_out); break;
@@ -497,6 +506,9 @@ hipError_t launch_real(const DevProb* probs, const int2* items, int n_items, int
     case 16: hipLaunchKernelGGL(k_real<16>, g, b, 0, st, probs, items, set, n_out); break;
     default: hipLaunchKernelGGL(k_real<0>, g, b, 0, st, probs, items, set, n_out);
   }
+#else
+  hipLaunchKernelGGL(k_real<0>, g, b, 0, st, probs, items, set, n_out);
+#endif
   return hipGetLastError();
 }
 

@@ -112,6 +112,11 @@ struct LaneGroup {
   // span_off in dse_ctx::d_span_items (tiles of one register 8 apart, padding items x = -1)
   int span_L = 0, span_rb = 0;
   int64_t span_off = 0, span_count = 0;
+  // launch boundaries inside those items (relative to span_off, last = span_count): whole blocks of
+  // 8 registers, each launch at most what the chip holds at once (every register's tiles resident
+  // together: its hand-offs wait on each other)
+  std::vector<int64_t> span_cuts;
+  std::vector<double> span_am, span_fl;  // per launch: amplitudes x terms, algorithmic flops
   // real-component registers: k_real over real_count items (problem, component) from real_off in
   // dse_ctx::d_real_items, then k_real_combine over real_np items (problem, 0) from real_poff
   bool real = false;
@@ -275,6 +280,7 @@ struct dse_ctx {
   // the two-stage eigensolver's cross-workgroup polls give up after this many rounds (option
   // eig_spin_limit; < 0: at once, tests); a give-up re-solves that register with dsyevd
   int eig_spin = kEig2DefaultSpin;
+  HandoffKnobs hk;  // options spin_limit, handoff_fences: every persistent launch of this context
   std::atomic<int> eig_fallbacks{0};  // registers re-solved that way in the last evolve
   // dense engine: eigenvalues refined by double-double Rayleigh quotients and output phases reduced
   // in double-double (option "dense_refine", default 1; 0: the eigensolver's eigenvalues and fp64
@@ -1378,10 +1384,10 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     if (!(value >= 1 && value <= 1e6)) return fail(ctx, DSE_ERR_ARG, "small_chunk must be in 1..1e6");
     ctx->small_chunk = (int)value;
   } else if (k == "handoff_fences") {  // interval kernel: agent release/acquire around each hand-off
-    HIPC(set_handoff_fences(value != 0.0));
+    ctx->hk.fences = value != 0.0;
   } else if (k == "spin_limit") {  // diagnostics: partner-flag polls per hand-off (< 0: always fail)
-    HIPC(set_spin_limit((int)value));
-    HIPC(set_span_spin_limit((int)value));
+    if (!(value >= -1 && value <= 1 << 30)) return fail(ctx, DSE_ERR_ARG, "spin_limit must be in -1..2^30");
+    ctx->hk.spin_limit = (int)value;
   } else if (k == "xcd_pairs") {
     ctx->xcd_pairs = value != 0.0;
   } else if (k == "span") {  // spanning registers: 0 off, 1..4 top bits (workgroups 2^s per register)
@@ -1404,13 +1410,14 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "time_kernels") {
     if (!(value >= 0)) return fail(ctx, DSE_ERR_ARG, "time_kernels must be >= 0");
     ctx->time_every = (int)value;
-  } else if (k == "ablate") {  // diagnostics only: skip kernel sections (results become wrong)
-    HIPC(set_ablate((int)value));
-    HIPC(set_ablate_interval((int)value));
-  } else if (k == "real_ablate") {  // diagnostics only: skip k_real sections (results become wrong)
-    HIPC(set_real_ablate((int)value));
-  } else if (k == "span_ablate") {  // diagnostics only: skip k_span sections (results become wrong)
-    HIPC(set_span_ablate((int)value));
+  } else if (k == "ablate" || k == "real_ablate" || k == "span_ablate") {
+    // diagnostics builds only (-DDSE_DIAG): skip kernel sections (results become wrong); process-wide
+    const int m = (int)value;
+    const hipError_t e = k == "ablate" ? (set_ablate(m) == hipSuccess ? set_ablate_interval(m) : hipErrorNotSupported)
+                         : k == "real_ablate" ? set_real_ablate(m) : set_span_ablate(m);
+    if (e == hipErrorNotSupported)
+      return fail(ctx, DSE_ERR_ARG, "option " + k + " needs a diagnostics build of libdse (-DDSE_DIAG)");
+    if (e != hipSuccess) return fail(ctx, DSE_ERR_ARG, "bad " + k + " mask");
   } else if (k == "probe_items") {  // diagnostics only: dse_time_step_kernel launches this many items
     ctx->probe_items = (int64_t)value;
   } else if (k == "max_degree") {
@@ -1864,16 +1871,19 @@ constexpr size_t kEig2MinDim = 8192;
 // s: 2.96e-13 dim^3 + 3.73e-9 dim^2 + 0.047).  The long reference grid (30 s, 20 000 outputs)
 // goes dense at every register size; the 1 ms head-to-head grid at N = 14 and config 2 (N = 12,
 // 2 ms) stay on Chebyshev.
-bool dense_cheaper(const HostProblem& P, const double* t, int n_t, bool half_eig) {
+bool dense_cheaper(const HostProblem& P, const double* t, int n_t, int eig_impl) {
   if (n_t < 2) return false;
   const double dim = std::ldexp(1.0, P.n_local);
   const double alpha = 0.5 * (P.e_max - P.e_min);
   const double terms = alpha * (t[n_t - 1] - t[0]) + 25.0 * (n_t - 1);
   const double cheb = terms * dim * (P.flops_per_amp > 0 ? P.flops_per_amp : 300.0) / 15e12;
-  double eig = half_eig && dim >= (double)kEigHalfMinDim
-                   ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
-                   : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
-  if (half_eig && dim >= 16384.0) eig *= 0.61;  // two-stage: 1.43 vs 2.35 s at 2^14
+  // the solver eig_impl takes for this size (dense_run's half_min / two_min)
+  const size_t d = (size_t)dim;
+  const size_t half_min = eig_impl == 1 ? kEigHalfMinDim : (eig_impl == 2 || eig_impl == 3) ? 1024 : SIZE_MAX;
+  const size_t two_min = eig_impl == 1 ? kEig2MinDim : eig_impl == 3 ? 1024 : SIZE_MAX;
+  double eig = d >= half_min ? 0.047 + 2.96e-13 * dim * dim * dim + 3.73e-9 * dim * dim
+                             : 1e-4 + 6.4e-13 * dim * dim * dim + 4.9e-9 * dim * dim + (dim >= 1024 ? 2e-2 : 0.0);
+  if (d >= two_min && dim >= 16384.0) eig *= 0.61;  // two-stage: 1.43 vs 2.35 s at 2^14 (level at 2^13)
   const double dense = eig + 4.0 * dim * dim * n_t / 40e12 + (double)n_t * dim * P.n_local * 32.0 / 2e12;
   return dense < cheb;
 }
@@ -2077,10 +2087,10 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         half_min = SIZE_MAX;
       }
     }
-    // the workers take tasks largest first; every solved register (a batched task: its whole job)
-    // goes to the output queue at once, and this thread runs its output GEMMs (dense_stream) while
-    // the other registers' solves go on (round 4 queued a job only when all its registers were
-    // solved, so a round's 2^14 outputs waited for its last 2^14 solve)
+    // the workers take tasks largest first; a job whose last register is solved goes to the output
+    // queue, and this thread runs its output GEMMs (dense_stream) while the other solves go on
+    // (outputs per register as each solve ends measured the same: 3.51-3.56 s per N = 14 point
+    // either way over 16 points, profiles/r05/fullsweep_outputs_ab.jsonl)
     std::atomic<size_t> next{0};
     std::atomic<bool> abort_all{false};
     std::vector<rocblas_status> wst(K, rocblas_status_success);
@@ -2089,6 +2099,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     std::mutex qm;
     std::condition_variable qcv;
     std::deque<Task> ready;
+    std::map<DenseJob*, int> pending;  // per job (dense_early 0): its registers not yet solved
+    for (const Task& T : tasks) pending[T.j] += 1;
     int workers_left = K;
     auto e1 = e0;
     auto worker = [&](int w) {
@@ -2133,8 +2145,10 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           break;
         }
         std::lock_guard<std::mutex> lk(qm);
-        ready.push_back(T);
-        qcv.notify_one();
+        if (--pending[&J] == 0) {
+          ready.push_back(Task{&J, -1});  // the whole job
+          qcv.notify_one();
+        }
       }
       std::lock_guard<std::mutex> lk(qm);
       if (--workers_left == 0) e1 = std::chrono::steady_clock::now();
@@ -2184,7 +2198,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     for (int w = 0; w < K; ++w) th.emplace_back(worker, w);
     int orc = DSE_OK;
     size_t done = 0;
-    while (done < tasks.size()) {
+    const size_t n_out_tasks = jobs.size();
+    while (done < n_out_tasks) {
       Task T{nullptr, 0};
       {
         std::unique_lock<std::mutex> lk(qm);
@@ -2210,7 +2225,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       if (wrc[w] != 0)
         return fail(ctx, DSE_ERR_HIP, "half-matrix eigensolver failed (step " + std::to_string(-wrc[w]) + ")");
     }
-    if (done < tasks.size()) return fail(ctx, DSE_ERR_HIP, "dense engine: eigensolver workers stopped early");
+    if (done < n_out_tasks) return fail(ctx, DSE_ERR_HIP, "dense engine: eigensolver workers stopped early");
     eig_ms += std::chrono::duration<double, std::milli>(e1 - e0).count();
   }
   if (ms_all) *ms_all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
@@ -2384,7 +2399,7 @@ int matrix_run(dse_ctx* ctx, int pi, const double* t, int n_t, double dt, double
     HIPC(hipMemcpyAsync(d_items, items.data(), dim * sizeof(int2), hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_init, init.data(), dim * sizeof(BasisInit), hipMemcpyHostToDevice, st));
     HIPC(launch_basis_init(d_init, (int)dim, dim, st));
-    HIPC(launch_interval(P.L, P.imag, d_p, d_items, (int)dim, 0, 0, 1, d_err, d_err, st, (long)dim));
+    HIPC(launch_interval(P.L, P.imag, d_p, d_items, (int)dim, 0, 0, 1, d_err, d_err, ctx->hk, st, (long)dim));
   }
   HIPC(hipEventRecord(mev[1], st));
   // psi_0 = e_x0, psi_1 = U e_x0 (column x0), psi_{j+1} = U psi_j
@@ -2693,7 +2708,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // dense engine first (option "dense"): a register it takes is off every Chebyshev path
   bool any_small = false, any_big = false, any_dense = false;
   for (auto& P : ctx->probs) {
-    P.dn = ctx->dense && dense_eligible(P) && (ctx->dense == 2 || dense_cheaper(P, t, n_t, ctx->eig_impl != 0));
+    P.dn = ctx->dense && dense_eligible(P) && (ctx->dense == 2 || dense_cheaper(P, t, n_t, ctx->eig_impl));
     any_dense = any_dense || P.dn;
   }
   for (auto& P : ctx->probs) {
@@ -3238,16 +3253,34 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
           if (pis.empty() || pis.back() != e.x) pis.push_back(e.x);
         }
         g.span_off = (int64_t)sitems.size();
+        int per_cu = 1;
+        HIPC(span_occupancy(g.span_L, g.span_rb, imag_all, &per_cu));
+        const int64_t resident = (int64_t)std::max(1, per_cu) * ctx->n_cu;
+        g.span_cuts.assign(1, 0);
+        g.span_am.assign(1, 0.0);
+        g.span_fl.assign(1, 0.0);
         for (size_t b0 = 0; b0 < pis.size(); b0 += 8) {
           int s = 0;  // the block's widest register sets its size (span_tile mixes 13 and 14 qubits)
           for (size_t i = b0; i < std::min(pis.size(), b0 + 8); ++i) s = std::max(s, ctx->probs[pis[i]].span_s);
           const size_t base = sitems.size();
+          if ((int64_t)(base + ((size_t)8 << s)) - g.span_off - g.span_cuts.back() > resident &&
+              (int64_t)base - g.span_off > g.span_cuts.back()) {
+            g.span_cuts.push_back((int64_t)base - g.span_off);  // this block starts the next launch
+            g.span_am.push_back(0.0);
+            g.span_fl.push_back(0.0);
+          }
+          for (size_t i = b0; i < std::min(pis.size(), b0 + 8); ++i) {
+            const HostProblem& P = ctx->probs[pis[i]];
+            g.span_am.back() += std::ldexp(1.0, P.n_local) * P.degree;
+            g.span_fl.back() += std::ldexp(1.0, P.n_local) * P.degree * P.flops_per_amp;
+          }
           sitems.resize(base + ((size_t)8 << s), make_int2(-1, 0));
           for (size_t i = b0; i < std::min(pis.size(), b0 + 8); ++i)
             for (int h = 0; h < (1 << ctx->probs[pis[i]].span_s); ++h)
               sitems[base + (size_t)h * 8 + (i - b0)] = make_int2(pis[i], h);
         }
         g.span_count = (int64_t)sitems.size() - g.span_off;
+        g.span_cuts.push_back(g.span_count);
       }
     // real-component groups: items (problem, component) in degree order, then (problem, 0) per
     // problem for the combine launch
@@ -3362,7 +3395,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       // co-resident chunk and group (persistent); records beyond the pool are skipped, not timed
       size_t need = 1;
       for (const auto& g : ln.groups)
-        need += persistent ? (size_t)((g.count + cap - 1) / cap) : (size_t)(ln.max_deg + 1);
+        need += persistent ? (g.tiles < 0 ? g.span_cuts.size() - 1 : (size_t)((g.count + cap - 1) / cap))
+                           : (size_t)(ln.max_deg + 1);
       if ((rc = ensure_events(ctx, ln, need))) return rc;
     }
 
@@ -3447,20 +3481,30 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
             if (g.real)
               return launch_real(ctx->d_probs, ctx->d_real_items + g.real_off, (int)g.real_count, set, G.n_out,
                                  ln.stream);
-            if (g.tiles < 0)
-              return launch_span(g.span_L, g.span_rb, imag_all, ctx->d_probs, ctx->d_span, ctx->d_span_items + g.span_off,
-                                 (int)g.span_count, q, set, G.n_out, d_err, ln.stream);
+            if (g.tiles < 0)  // chunk [off, off + cnt) of the group's span launches
+              return launch_span(g.span_L, g.span_rb, imag_all, ctx->d_probs, ctx->d_span,
+                                 ctx->d_span_items + g.span_off + g.span_cuts[off],
+                                 (int)(g.span_cuts[off + cnt] - g.span_cuts[off]), q, set, G.n_out, d_err, ctx->hk,
+                                 ln.stream);
             return launch_interval(g.L, imag_all, ctx->d_probs, ctx->d_items_iv + g.off + off, cnt, q, set, G.n_out,
-                                   ctx->d_flags, d_err, ln.stream);
+                                   ctx->d_flags, d_err, ctx->hk, ln.stream);
           };
-          const int64_t gcap = g.tiles == 2 ? cap : g.count;  // mixed (0), span (< 0): one launch
-          for (int64_t off = 0; off < g.count; off += gcap) {
-            const int cnt = (int)std::min<int64_t>(gcap, g.count - off);
+          // mixed (0): one launch; 2-tile: co-resident chunks of cap items; span (< 0): one launch
+          // per chunk of span_cuts (off / cnt then count chunks, not items)
+          const int64_t gcap = g.tiles == 2 ? cap : g.tiles < 0 ? 1 : g.count;
+          const int64_t gn = g.tiles < 0 ? (int64_t)g.span_cuts.size() - 1 : g.count;
+          for (int64_t off = 0; off < gn; off += gcap) {
+            const int cnt = (int)std::min<int64_t>(gcap, gn - off);
             double fl = 0.0, am = 0.0;
-            for (int64_t i = off; i < off + cnt; ++i) {
-              const HostProblem& P = ctx->probs[items[g.off + i].x];
-              am += (double)T * P.degree;
-              fl += (double)T * P.degree * P.flops_per_amp;
+            if (g.tiles < 0) {  // the chunk's registers
+              am = g.span_am[off];
+              fl = g.span_fl[off];
+            } else {
+              for (int64_t i = off; i < off + cnt; ++i) {
+                const HostProblem& P = ctx->probs[items[g.off + i].x];
+                am += (double)T * P.degree;
+                fl += (double)T * P.degree * P.flops_per_amp;
+              }
             }
             if (timed && 2 * ln.ev_used[pool] + 2 <= ln.ev[pool].size()) {
               const size_t i = ln.ev_used[pool]++;

@@ -35,20 +35,19 @@
 
 namespace dse {
 
-// Polls of the partners' flags before a hand-off is declared failed (s_sleep 1 between polls);
-// negative: fail at once (diagnostics: exercises the fallback)
-__device__ int g_span_spin_limit = 1 << 22;
-// Diagnostic ablation mask (0 in production; results are wrong otherwise): 1 no pre-pass, 2 no
-// publish, 4 no poll, 8 no operand loads, 16 no propagator sums, 32 no fused loop, 64 no raw store
+// Diagnostic ablation mask (diagnostics builds, -DDSE_DIAG; 0 in libdse.so; results are wrong
+// otherwise): 1 no pre-pass, 2 no publish, 4 no poll, 8 no operand loads, 16 no propagator sums, 32
+// no fused loop, 64 no raw store.  The partners' flags are polled HandoffKnobs::spin_limit times
+// (a kernel argument, per context) before a hand-off is declared failed; negative: fail at once.
+#ifdef DSE_DIAG
 __device__ int g_span_ablate = 0;
-
 hipError_t set_span_ablate(int mask) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_span_ablate), &mask, sizeof(int));
 }
-
-hipError_t set_span_spin_limit(int limit) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_span_spin_limit), &limit, sizeof(int));
-}
+#else
+constexpr int g_span_ablate = 0;
+hipError_t set_span_ablate(int mask) { return mask ? hipErrorNotSupported : hipSuccess; }
+#endif
 
 namespace {
 
@@ -110,7 +109,7 @@ struct SpanShared {
 template <int L, int RB, bool IMAG>
 __global__ void __launch_bounds__(1 << (L - RB))
 k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
-       const int2* __restrict__ items, int q, int set, int n_out, int* __restrict__ err) {
+       const int2* __restrict__ items, int q, int set, int n_out, int* __restrict__ err, HandoffKnobs hk) {
   using G = SpanGeo<L, RB>;
   constexpr int R = G::R, TB = G::TB, NT = G::NT, IW = G::IW, NPI = G::NPI, US = G::US;
   // 1024-thread tiles run 4 waves per SIMD (<= 128 VGPRs): fewer operands in flight, propagator
@@ -383,7 +382,7 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
         const bool ok = !need || __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= k;
         if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > g_span_spin_limit ||
+        if (++spins > hk.spin_limit ||
             ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
           if (lane == 0) {
             S.fail = 1;
@@ -510,16 +509,16 @@ hipError_t span_occupancy(int L, int RB, bool imag, int* blocks_per_cu) {
 
 hipError_t launch_span(int L, int RB, bool imag, const DevProb* probs, const SpanDesc* sdesc,
                        const int2* items, int n_items, int q, int set, int n_out, int* err,
-                       hipStream_t st) {
+                       HandoffKnobs hk, hipStream_t st) {
   if (n_items <= 0) return hipSuccess;
 #define X(l, rb)                                                                                   \
   if (L == l && RB == rb) {                                                                        \
     if (imag)                                                                                      \
       hipLaunchKernelGGL((k_span<l, rb, true>), dim3(n_items), dim3(SpanGeo<l, rb>::NT), 0, st,   \
-                         probs, sdesc, items, q, set, n_out, err);                                 \
+                         probs, sdesc, items, q, set, n_out, err, hk);                             \
     else                                                                                           \
       hipLaunchKernelGGL((k_span<l, rb, false>), dim3(n_items), dim3(SpanGeo<l, rb>::NT), 0, st,  \
-                         probs, sdesc, items, q, set, n_out, err);                                 \
+                         probs, sdesc, items, q, set, n_out, err, hk);                             \
     return hipGetLastError();                                                                      \
   }
   DSE_SPAN_CONFIGS(X)

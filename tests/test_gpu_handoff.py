@@ -172,3 +172,50 @@ def test_span_handoff_failure_falls_back(engine):
         engine.clear()
     assert st2["handoff_fallbacks"] >= 1
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12)
+
+
+def test_explicit_span_beyond_the_chip_runs_in_resident_chunks(engine):
+    """span_tile = 11 on 48 fourteen-qubit registers: 384 spanning workgroups, more than the chip
+    holds at once.  The runtime cuts the group into launches of whole 8-register blocks that fit
+    (every register's tiles resident together), so no hand-off waits on a queued partner: no
+    fallback, and the results are k_interval's."""
+    t = np.linspace(0.0, 1e-4, 11)
+    probs = [pb.build_problem(sweep_point_params(13, float(d), v, 1e-4, 11))
+             for d in np.linspace(0.0, 150e3, 24) for v in ("center_on", "shell_off")]
+    ref, st0, _ = _run_states(engine, probs, t)
+    assert st0["span_problems"] == 0
+    engine.set_option("span_tile", 11)
+    try:
+        got, st, _ = _run_states(engine, probs, t)
+    finally:
+        engine.set_option("span_tile", 0)
+        engine.clear()
+    assert st["span_problems"] == len(probs) and st["handoff_fallbacks"] == 0
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-11)
+
+
+def test_handoff_options_are_per_context(engine):
+    """spin_limit (and handoff_fences) are context options passed with every launch, not
+    process-wide settings: a second context that fails every hand-off (spin_limit = -1) leaves
+    this context's evolve on the persistent kernel with no fallback."""
+    from quantumsimulations_amd.engine import Engine
+    probs = _two_tile_problems()
+    other = Engine(0)
+    try:
+        other.set_option("real", 0)
+        other.set_option("span_tile", 0)
+        other.set_option("spin_limit", -1)
+        for p in probs:
+            other.add(p)
+        engine.clear()
+        for p in probs:
+            engine.add(p)
+        ref, st = engine.evolve(T)
+        _, st_o = other.evolve(T)
+        again, st2 = engine.evolve(T)
+    finally:
+        other.close()
+        engine.clear()
+    assert st["handoff_fallbacks"] == 0 and st2["handoff_fallbacks"] == 0 and st2["mode"] == 1
+    assert st_o["handoff_fallbacks"] >= 1
+    assert np.array_equal(again, ref)

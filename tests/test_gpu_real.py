@@ -1,4 +1,5 @@
-"""The real-component mode (dse_real.hip, option "real", default): with imaginary drives the rotated
+"""The real-component mode (dse_real.hip, option "real" = 1, or 2 for the 14-qubit registers only;
+default 0 = the complex kernels): with imaginary drives the rotated
 Hamiltonian H' = D H D^dagger is real symmetric, and the rotated state's real and imaginary parts
 run as two independent real Chebyshev recurrences, one workgroup each holding the whole register
 in LDS.  Checked against the persistent complex kernel k_interval (option real = 0) -- both exact

@@ -1,5 +1,9 @@
 """Debug: run-to-run determinism of the persistent 2-tile path under kernel-section ablations.
-Prints, per ablation mask, the largest deviation between repeated evolves of the same problems."""
+Prints, per ablation mask, the largest deviation between repeated evolves of the same problems.
+Ablation options (ablate, span_ablate, real_ablate) need a diagnostics build of the same ABI:
+    DSE_EXTRA_FLAGS=-DDSE_DIAG python -m quantumsimulations_amd.build --out tools/bin/libdse_diag.so
+    DSE_LIB=tools/bin/libdse_diag.so python3 tools/dbg_parity.py ...
+"""
 import sys, numpy as np
 sys.path.insert(0, '.')
 from quantumsimulations_amd import problem as pb

@@ -26,7 +26,7 @@ def main():
     t_ref = np.linspace(0.0, 30.0, 20000)
     with Engine(0) as eng:
         for settings in sys.argv[1:] or [""]:
-            opts = dict(kv.split("=") for kv in settings.split(",") if kv)
+            opts = dict(kv.split("=") for kv in settings.replace("+", ",").split(",") if kv)
             npts = int(opts.pop("points", 0))
             dets = np.linspace(0.0, 150e3, npts) if npts else [50e3]
             probs = [pb.build_problem(sweep_point_params(13, float(d), v, 30.0, 20000)) for d in dets for v in VARIANTS]

@@ -5,6 +5,10 @@
 
 One output interval (dt = 1e-5 s) of the 64-point N = 14 sweep per configuration; prints the
 HIP-event time of each lane's k_interval launch.  Ablated runs compute wrong numbers on purpose.
+
+Ablation options (ablate, span_ablate, real_ablate) need a diagnostics build of the same ABI:
+    DSE_EXTRA_FLAGS=-DDSE_DIAG python -m quantumsimulations_amd.build --out tools/bin/libdse_diag.so
+    DSE_LIB=tools/bin/libdse_diag.so python3 tools/probe_interval.py ...
 """
 from __future__ import annotations
 

@@ -7,6 +7,10 @@
     python3 tools/probe_span.py shard [reps]    one GPU's share of the 64-point sweep on 8 GPUs
                                                 (8 points = 24 evolutions), default / span_tile 11 / 10
 Grid: config 3's 1 ms / 101 outputs.  Kernel time = HIP events around every interval launch.
+
+Ablation options (ablate, span_ablate, real_ablate) need a diagnostics build of the same ABI:
+    DSE_EXTRA_FLAGS=-DDSE_DIAG python -m quantumsimulations_amd.build --out tools/bin/libdse_diag.so
+    DSE_LIB=tools/bin/libdse_diag.so python3 tools/probe_span.py ...
 """
 import json
 import os

@@ -5,6 +5,10 @@
 
 Prints one JSON line per configuration (mean launch time, GB/s of the algorithmic bytes).
 Ablated runs compute wrong numbers on purpose; this never touches parity.
+
+Ablation options (ablate, span_ablate, real_ablate) need a diagnostics build of the same ABI:
+    DSE_EXTRA_FLAGS=-DDSE_DIAG python -m quantumsimulations_amd.build --out tools/bin/libdse_diag.so
+    DSE_LIB=tools/bin/libdse_diag.so python3 tools/probe_step.py ...
 """
 from __future__ import annotations
 
