@@ -39,6 +39,7 @@ struct DenseProb {
   double* lam;          // [dim] eigenvalues (ascending); after k_dense_rq the high part of each
                         // refined eigenvalue (double-double lam + lam_lo)
   double* lam_lo;       // [dim] low parts (zero without the refinement)
+  double* diag_dd;      // [2 dim] the exact diagonal <x|H'|x> as double-double (hi, lo), for k_dense_rq
   double* obs;          // [n_t][8] raw observable sums of this problem (finish_obs order)
   double2* final_state; // [dim] psi(t_last) in the reference frame (dse_get_state), or null
 };
@@ -49,6 +50,7 @@ hipError_t launch_dense_h(const DenseProb* d, int count, int dim, hipStream_t st
 // / v_a^T v_a with H' applied from the coefficient tables (the same fp64 matrix k_dense_h built).
 // The eigensolver's eigenvalues carry errors ~eps ||H'|| sqrt(dim) (a phase error growing like that
 // times t); the quotient of its eigenvector is exact to ~(eps ||H'||)^2 / gap + eps^2 ||H'||.
+// (launch_dense_rq first writes diag_dd: one exact diagonal per row, not one per row and column)
 hipError_t launch_dense_rq(const DenseProb* d, int count, int dim, hipStream_t st);
 // phase columns of output times tau[0 .. tb): P[a + j dim] = c_a cos(lambda_a tau_j),
 // P[a + (tb + j) dim] = -c_a sin(lambda_a tau_j); problem p's block at P + p * pstride

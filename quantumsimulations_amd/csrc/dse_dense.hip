@@ -119,6 +119,17 @@ __device__ __forceinline__ ddv dense_diag_dd(const DenseProb& P, uint32_t x) {
   return d;
 }
 
+// the exact diagonal of every row, once (k_dense_rq reads it for every eigenvector)
+__global__ void __launch_bounds__(256)
+k_dense_diag(const DenseProb* __restrict__ probs, int dim) {
+  const DenseProb& P = probs[blockIdx.y];
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (x >= (uint32_t)dim) return;
+  const ddv d = dense_diag_dd(P, x);
+  P.diag_dd[2 * (size_t)x] = d.hi;
+  P.diag_dd[2 * (size_t)x + 1] = d.lo;
+}
+
 // Rayleigh quotient of eigenvector a (column a of V) in double-double: one workgroup per
 // (eigenvector, problem); thread partials summed in a fixed order (deterministic)
 __global__ void __launch_bounds__(256)
@@ -127,10 +138,12 @@ k_dense_rq(const DenseProb* __restrict__ probs, int dim) {
   const DenseProb& P = probs[blockIdx.y];
   const uint32_t a = blockIdx.x;
   const double* v = P.V + (size_t)a * dim;
+  const double2* dg = reinterpret_cast<const double2*>(P.diag_dd);
   ddv num = {0.0, 0.0}, den = {0.0, 0.0};
   for (uint32_t x = threadIdx.x; x < (uint32_t)dim; x += 256u) {
     const double vx = v[x];
-    ddv y = dd_mul_d(dense_diag_dd(P, x), vx);
+    const double2 dx = dg[x];
+    ddv y = dd_mul_d(ddv{dx.x, dx.y}, vx);
     dense_offdiag(P, x, [&](uint32_t yy, double c) { y = dd_add(y, dd_prod(c, v[yy])); });
     num = dd_add(num, dd_mul_d(y, vx));
     den = dd_add(den, dd_prod(vx, vx));
@@ -287,6 +300,7 @@ hipError_t launch_dense_h(const DenseProb* d, int count, int dim, hipStream_t st
 }
 
 hipError_t launch_dense_rq(const DenseProb* d, int count, int dim, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_diag, dim3((dim + 255) / 256, count), dim3(256), 0, st, d, dim);
   hipLaunchKernelGGL(k_dense_rq, dim3(dim, count), dim3(256), 0, st, d, dim);
   return hipGetLastError();
 }

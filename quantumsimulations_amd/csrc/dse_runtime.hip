@@ -1916,6 +1916,7 @@ struct DenseJob {
   std::vector<int> list;  // problem indices
   DevArena ba;
   double *V = nullptr, *lam = nullptr, *lam_lo = nullptr, *E = nullptr, *Pm = nullptr, *Psi = nullptr, *obs = nullptr;
+  double* diag_dd = nullptr;
   rocblas_int* info = nullptr;
   DenseProb* d_desc = nullptr;
 };
@@ -1963,7 +1964,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       // outputs per block: P and Psi' of a problem take 2 x dim x 2 TB doubles (<= 256 MiB each)
       const int TB = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_t, (size_t(256) << 20) / (16 * dim)));
       const size_t pstride = dim * 2 * (size_t)TB;
-      const double per = (double)((dim * dim + 2 * pstride + 3 * dim + (size_t)n_t * 8 + 2 * n * n + 4 * n) * sizeof(double));
+      const double per = (double)((dim * dim + 2 * pstride + 5 * dim + (size_t)n_t * 8 + 2 * n * n + 4 * n) * sizeof(double));
       size_t same = 0;
       while (idx + same < order.size() && ctx->probs[order[idx + same]].n_local == n) ++same;
       size_t cnt = (size_t)std::max(0.0, (budget - used) / per);
@@ -1976,6 +1977,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       J->V = ba.get<double>(dim * dim * cnt);
       J->lam = ba.get<double>(dim * cnt);
       J->lam_lo = ba.get<double>(dim * cnt);
+      J->diag_dd = ba.get<double>(2 * dim * cnt);
       J->E = ba.get<double>(dim * cnt);
       J->info = ba.get<rocblas_int>(cnt);
       J->Pm = ba.get<double>(pstride * cnt);
@@ -1984,7 +1986,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       const size_t tsz = (size_t)(2 * n * n + 5 * n);
       double* tabs = ba.get<double>(tsz * cnt);
       J->d_desc = ba.get<DenseProb>(cnt);
-      if (!J->V || !J->lam || !J->lam_lo || !J->E || !J->info || !J->Pm || !J->Psi || !J->obs || !tabs || !J->d_desc) {
+      if (!J->V || !J->lam || !J->lam_lo || !J->diag_dd || !J->E || !J->info || !J->Pm || !J->Psi || !J->obs || !tabs || !J->d_desc) {
         if (!jobs.empty()) break;  // this round is full: the register waits for the next one
         return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed (dim " + std::to_string(dim) + ")");
       }
@@ -2013,6 +2015,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         D.V = J->V + dim * dim * i;
         D.lam = J->lam + dim * i;
         D.lam_lo = J->lam_lo + dim * i;
+        D.diag_dd = J->diag_dd + 2 * dim * i;
         D.refine = ctx->dense_refine;
         D.obs = J->obs + (size_t)n_t * 8 * i;
         D.final_state = P.buf[0];

@@ -64,7 +64,9 @@ struct SpanGeo {
   static constexpr int NPI = (TB * (TB - 1) / 2 + TB - 1) / TB;  // thread pairs per iteration
   static constexpr int IW = 4 + NPI;                   // dv2 per iteration row
   static constexpr uint32_t TBYTES = (16u << L);
-  static constexpr int US = (R <= 4 && NT < 1024) ? 4 : 2;  // u operands built per pre-pass sweep
+  // u operands built per pre-pass sweep (2^11-amplitude tiles have at most 3 top bits at n <= 14,
+  // and 3 keeps the pipelined pre-pass inside the register budget there)
+  static constexpr int US = (R <= 4 && NT < 1024) ? (TB >= 9 ? 3 : 4) : 2;
 };
 
 template <bool IMAG>
@@ -103,6 +105,11 @@ struct SpanShared {
   using G = SpanGeo<L, RB>;
   dv2 w[2][1 << L];        // w_{k-1} and w_k (double buffer)
   dv2 it[G::TB][G::IW];    // iteration rows
+  // the u pre-pass's coefficients by operand slot c (the c-th top bit with a u operand): g_{j,b}
+  // of the tile bits, the top bit's drive at the partner's bit value, that value (0 / 1)
+  double ug[kSpanMaxTop][16];
+  double uf[kSpanMaxTop][2];
+  double ucb[kSpanMaxTop];
   int fail;
 };
 
@@ -163,6 +170,16 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
   {
     const gd2* src = (const gd2*)D.tab->it;
     for (int e = tid; e < TB * IW; e += NT) (&S.it[0][0])[e] = src[e];
+    if (tid < kSpanMaxTop * 16) {  // u operand slots c < n_u (LDS broadcast reads in the pre-pass)
+      const int c = tid >> 4, j = tid & 15;
+      if (c < n_u) {
+        const int b = ubit_of(c);
+        const int v = (int)(((h >> b) & 1u) ^ 1u);  // the consumer's (partner's) value of bit b
+        S.ug[c][j] = j < L ? tab->ug[b][j] : 0.0;
+        if (j < 2) S.uf[c][j] = tab->uflip[b][2 * v + j];
+        if (j == 0) S.ucb[c] = (double)v;
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -218,47 +235,43 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
     auto prepass = [&](auto nu_tag, int c0) {
       constexpr int NU = decltype(nu_tag)::value;
       double2 u[NU][R];
-      int ubit[NU];
       double cb[NU];  // the consumer's value of bit b (the partner's: 1 - h_b)
 #pragma unroll
       for (int bb = 0; bb < NU; ++bb) {
-        const int b = ubit_of(c0 + bb);
-        ubit[bb] = b;
-        cb[bb] = (double)(((h >> b) & 1u) ^ 1u);
-        const int v = (int)cb[bb];
-        const double fr = tab->uflip[b][2 * v], fi = tab->uflip[b][2 * v + 1];
+        const int c = c0 + bb;
+        cb[bb] = S.ucb[c];
+        const double fr = S.uf[c][0], fi = S.uf[c][1];
 #pragma unroll
         for (int r = 0; r < R; ++r) u[bb][r] = smad<IMAG>(make_double2(0.0, 0.0), fr, fi, own[r]);
         // register bits: output rows with r_i == c, source r ^ e_i
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
-          const double g = tab->ug[b][TB + i];
+          const double g = S.ug[c][TB + i];
 #pragma unroll
           for (int r = 0; r < R; ++r) rfma(u[bb][r], ((double)((r >> i) & 1) == cb[bb]) ? g : 0.0, own[r ^ (1 << i)]);
         }
       }
-#pragma unroll 1
-      for (int j = 0; j < TB; ++j) {
-        double gj[NU];
-        bool any = false;
+      // thread bits, software-pipelined (round 5: the rows of bit j + 1 in flight under bit j's
+      // FMAs, the coefficients LDS broadcasts staged at setup; the round-4 loop waited on a scalar
+      // load and an LDS read every iteration: 2.3 of the 10.0 us term of a lone register)
+      auto bit_terms = [&](int j, const double2* pv) {
         const double tj = (double)((tid >> j) & 1);
 #pragma unroll
         for (int bb = 0; bb < NU; ++bb) {
-          const double g = tab->ug[ubit[bb]][j];
-          gj[bb] = (tj == cb[bb]) ? g : 0.0;
-          any = any || gj[bb] != 0.0;
+          const double gj = (tj == cb[bb]) ? S.ug[c0 + bb][j] : 0.0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) rfma(u[bb][r], gj, pv[r]);
         }
-        if (j >= 6 && !__builtin_amdgcn_readfirstlane((int)any)) continue;  // a wave bit: no lane uses it
+      };
+#pragma unroll 1
+      for (int j = 0; j < TB; ++j) {
         double2 pv[R];
         rows_lds<NT, R>(cur, tid ^ (1 << j), pv);
-#pragma unroll
-        for (int bb = 0; bb < NU; ++bb)
-#pragma unroll
-          for (int r = 0; r < R; ++r) rfma(u[bb][r], gj[bb], pv[r]);
+        bit_terms(j, pv);
       }
 #pragma unroll
       for (int bb = 0; bb < NU; ++bb) {
-        const __amdgpu_buffer_rsrc_t dst = tile_rsrc(slot_ptr(h, ubit[bb], (k - 1) % kXSlots), TBYTES);
+        const __amdgpu_buffer_rsrc_t dst = tile_rsrc(slot_ptr(h, ubit_of(c0 + bb), (k - 1) % kXSlots), TBYTES);
 #pragma unroll
         for (int r = 0; r < R; ++r) bst<kSc1>(dst, voff, (uint32_t)(r * NT * 16), u[bb][r]);
       }
@@ -272,7 +285,9 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
         else prepass(std::integral_constant<int, (US >= 4 ? 4 : 1)>{}, c0);
       }
     }
-    // ---- phase 1: diagonal, register-bit drives and pairs ----
+    // ---- phase 1: diagonal, register-bit drives and pairs (own rows re-read: not held across the
+    // pre-pass, whose operands and pipelined partner rows take those registers) ----
+    if (n_u > 0) rows_lds<NT, R>(cur, tid, own);
     double2 out[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) out[r] = make_double2(dg[r] * own[r].x, dg[r] * own[r].y);
