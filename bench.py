@@ -115,7 +115,7 @@ def parse():
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command (tools/gpu.sh traffic +
 # tools/pmc_summary.py), newest round first
 PMC_TRAFFIC = [os.path.join(ROOT, "profiles", r, f) for r, f in
-               (("r04", "bench_pmc_traffic.json"), ("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
+               (("r05", "bench_pmc_traffic.json"), ("r04", "bench_pmc_traffic.json"), ("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
                 ("r01", "v9_pmc_traffic.json"))]
 
 
@@ -159,7 +159,7 @@ def cpu_baseline(fraction: float, cores: int):
 
 
 WHT_PMC_N30 = next((q for q in (os.path.join(ROOT, "profiles", r, "wht_n30_pmc_traffic.json")
-                                 for r in ("r04", "r01")) if os.path.exists(q)),
+                                 for r in ("r05", "r04", "r01")) if os.path.exists(q)),
                    os.path.join(ROOT, "profiles", "r01", "wht_n30_pmc_traffic.json"))
 
 

@@ -2,7 +2,7 @@
 """Per-kernel HBM-side traffic from the FETCH_SIZE / WRITE_SIZE counter passes of
 tools/gpu_profile.sh (gpurun_out/prof/{fetch,write}/*_counter_collection.csv) -> JSON.
 
-    python tools/pmc_summary.py gpurun_out/prof profiles/r01/v7_pmc_traffic.json
+    python tools/pmc_summary.py gpurun_out/prof profiles/r01/v7_pmc_traffic.json ["<profiled command>"]
 
 rocprofv3 reports kB per dispatch.  FETCH_SIZE is doubled: on gfx950 it counts 1/2 of a wide
 (16 B per lane) streaming read (MI355X_MICROARCH.md, HBM section); WRITE_SIZE as reported.
@@ -28,6 +28,7 @@ def per_kernel(path):
 
 def main():
     root, out = sys.argv[1], sys.argv[2]
+    cmd = sys.argv[3] if len(sys.argv) > 3 else "python3 bench.py --no-cpu-baseline --steps 1 --warmup 0"
     fe = per_kernel(root + "/fetch/*counter_collection.csv")
     wr = per_kernel(root + "/write/*counter_collection.csv")
     kernels = {}
@@ -38,7 +39,7 @@ def main():
                       "write_bytes": w, "traffic_bytes_per_launch": 2 * f + w}
     rec = {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, over "
-                  "`python3 bench.py --no-cpu-baseline --steps 1 --warmup 0` (tools/gpu_profile.sh)",
+                  f"`{cmd}` (tools/gpu.sh traffic / traffic_large)",
         "units": "bytes per launch (rocprofv3 reports kB)",
         "gfx950_correction": "FETCH_SIZE doubled: it counts 1/2 of a wide (16 B/lane) streaming read on "
                              "gfx950 (MI355X_MICROARCH.md, HBM section); WRITE_SIZE as reported",
