@@ -213,6 +213,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         qubits and all their tiles fit the chip at once, else none; 0 never
  *          "span"         the same with a fixed number s = 1..4 of top bits per register
  *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
+ *          "span_outputs" outputs per launch (1..4, default 4) of an evolve whose registers all
+ *                         span: k_span staggers the outputs' sums over the terms, so more
+ *                         outputs per Chebyshev series cost no extra registers
  *          "eig_spin_limit"  two-stage eigensolver: rounds a poll of another workgroup's result
  *                         waits before it gives up (default 2^22, ~0.1 s); a give-up voids that
  *                         solve and the register is re-solved by rocSOLVER dsyevd (stats

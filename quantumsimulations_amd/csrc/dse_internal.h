@@ -24,10 +24,8 @@ constexpr int kIvWaves = 8;                       // hand-off flags per tile (on
 #ifndef DSE_PIPE
 #define DSE_PIPE 1  // interval kernel: software-pipelined partner reads in the fused loop
 #endif
-#ifndef DSE_MAX_OUT
-#define DSE_MAX_OUT 2
-#endif
-constexpr int kMaxOut = DSE_MAX_OUT;              // output times per interval-kernel launch
+constexpr int kMaxOut = 2;      // output times per launch of k_interval / k_real (sums in registers)
+constexpr int kSpanMaxOut = 4;  // output times per k_span launch (staggered sums, coef_nterm)
 constexpr int kMaxShardBits = 3;                  // partitioned registers: up to 8 shards
 constexpr int kMaxShards = 1 << kMaxShardBits;
 // bits above an L-bit tile for the largest register (34 qubits), at least the 32-bit tile index
@@ -209,13 +207,19 @@ hipError_t launch_real_init(const DevProb* probs, const int2* items, int n_items
 __host__ __device__ __forceinline__ const double2* coef_row(const DevProb& P, int set, int j) {
   return P.coef + ((size_t)set * P.n_acc + j) * (size_t)(P.kcap1 + 1);
 }
-// Terms accumulated at term k (see CoefK): 2 at k = 1 (a_0 w_0 + a_1 w_1), 3 every third term
-// (k - 1 = 0 mod 3: a_{k-2}, a_{k-1}, a_k), the r = (k - 1) mod 3 left over at k = d, else 0.
-__host__ __device__ __forceinline__ int coef_nterm(int k, int d) {
+// Terms accumulated into a propagator sum at term k (see CoefK), for the update phase ph (0..2):
+// 2 at k = 1 (a_0 w_0 + a_1 w_1); then at every k >= 2 with (k - 1 - ph) = 0 mod 3 the terms since
+// the previous update (3; at the first update of phase 1 / 2 one / two), and the terms left over at
+// k = d; else 0.  A term can reach w_{k-2}, w_{k-1}, w_k, so no gap exceeds 3.  Phase 0 is the
+// original schedule (updates at k = 1, 4, 7, ...); k_span staggers output j to phase j % 3, so at
+// most ceil(M / 3) of its M sums are read-modify-written in one term.
+__host__ __device__ __forceinline__ int coef_nterm(int k, int d, int ph = 0) {
   if (k > d) return 0;
   if (k == 1) return 2;
-  const int r = (k - 1) % 3;
-  return r == 0 ? 3 : (k == d ? r : 0);
+  const int t = ((k - 1 - ph) % 3 + 3) % 3;
+  int last = t == 0 ? k - 3 : k - t;  // the previous update of phase ph at k' >= 2, else 1
+  if (last < 2) last = 1;
+  return (t == 0 || k == d) ? k - last : 0;
 }
 // (scalar loads: the row is read-only during a launch and uniform across the workgroup)
 __device__ __forceinline__ CoefK coef_at(const double2* row, int k) {

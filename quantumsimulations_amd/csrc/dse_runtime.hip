@@ -191,6 +191,7 @@ struct dse_ctx {
   BasisInit* d_init = nullptr;      // psi(t0) list
   size_t init_cap = 0;
   int outputs_per_launch = 2;       // M of the interval kernel (dse_evolve picks 1 on coarse grids)
+  int span_outputs = 4;             // M when every register spans (k_span, staggered sums)
   int64_t probe_items = 0;          // 0: all items
   int time_every = 1;               // 0: no kernel timing; N: time intervals with m % N == 0
   double max_degree = 2e6;
@@ -1351,6 +1352,10 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     if (!(value >= 1 && value <= kMaxOut))
       return fail(ctx, DSE_ERR_ARG, "outputs_per_launch must be in 1.." + std::to_string(kMaxOut));
     ctx->outputs_per_launch = (int)value;
+  } else if (k == "span_outputs") {  // M of an evolve whose registers all span (k_span)
+    if (!(value >= 1 && value <= kSpanMaxOut))
+      return fail(ctx, DSE_ERR_ARG, "span_outputs must be in 1.." + std::to_string(kSpanMaxOut));
+    ctx->span_outputs = (int)value;
   } else if (k == "coresident") {  // diagnostics: workgroups per chunk of a 2-tile interval launch
     if (!(value == 0 || (value >= 2 && value <= 4096)))
       return fail(ctx, DSE_ERR_ARG, "coresident must be 0 or in 2..4096");
@@ -2812,8 +2817,15 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   for (int m = 0; m + 1 < n_t; ++m)
     for (auto& P : ctx->probs)
       if (!P.side()) max_z = std::max(max_z, 0.5 * (P.e_max - P.e_min) * (t[m + 1] - t[m]));
+  // k_span staggers its outputs' sums over the terms (coef_nterm phases), so an evolve whose
+  // registers all span takes up to kSpanMaxOut outputs per series (option span_outputs);
+  // k_interval and k_real update every output's sum in one term, from registers: at most two
+  bool all_span = true;
+  for (auto& P : ctx->probs)
+    if (!P.side()) all_span = all_span && P.span_s > 0 && !P.rl;
   int M = 1;
-  if (persistent && max_z < 400.0) M = std::max(1, std::min(ctx->outputs_per_launch, n_t - 1));
+  if (persistent && max_z < 400.0)
+    M = std::max(1, std::min(all_span ? ctx->span_outputs : ctx->outputs_per_launch, n_t - 1));
 
   // ---- groups of M consecutive output intervals -> coefficient sets (distinct offset lists) ----
   struct Group {

@@ -25,7 +25,8 @@
 //             (partner t ^ e_i ^ e_j, coefficient zero in lanes with x_i != x_j)
 //   phase 4   the cross-tile operands (SpanOp): poll the partner wave's flag, read its rows (sc1)
 //   phase 5   w_k = 2 (H - beta) w_{k-1} / alpha - w_{k-2}, the propagator sums of the launch's
-//             outputs (every third term, as dse_interval.hip), w_k -> the other LDS buffer and,
+//             up to kSpanMaxOut outputs (each every third term, output j on phase j % 3 so the
+//             read-modify-writes spread over the terms), w_k -> the other LDS buffer and,
 //             when some partner reads raw vectors, to this tile's raw slot
 // Ring of kXSlots slots per operand kind: slot (k - 1) % kXSlots carries the operand of term k,
 // rewritten kXSlots terms later, by when every reader has passed its flag of a later term.
@@ -161,9 +162,9 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
 
   const double* crow = (const double*)coef_row(P, set, 0);
   const size_t rstride = 2 * (size_t)(P.kcap1 + 1);
-  int dj[kMaxOut];
+  int dj[kSpanMaxOut];
 #pragma unroll
-  for (int j = 0; j < kMaxOut; ++j) dj[j] = j < n_out ? (int)crow[j * rstride] : 0;
+  for (int j = 0; j < kSpanMaxOut; ++j) dj[j] = j < n_out ? (int)crow[j * rstride] : 0;
 
   // ---- setup: iteration rows -> LDS, w_0 tile -> LDS buffer 0, per-row diagonal ----
   if (tid == 0) S.fail = 0;
@@ -371,21 +372,33 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(flag_me, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // ---- propagator-sum rows of this term, loaded now so their latency hides under phase 4 ----
-    bool upd[kMaxOut];
-    __amdgpu_buffer_rsrc_t accr[kMaxOut];
-    double2 av[kMaxOut][R];
+    // ---- propagator sums updating at term k.  Output j updates on phase j % 3 (coef_nterm), so
+    // outside the rare coincidence with an output's last term at most SL of the launch's sums are
+    // read-modify-written per term; their rows are loaded now so the latency hides under phase 4 ----
+    constexpr int SL = (kSpanMaxOut + 2) / 3;
+    uint32_t um = 0, ntp = 0;  // outputs updating at term k; their term counts, 2 bits each (uniform)
 #pragma unroll
-    for (int j = 0; j < kMaxOut; ++j) {
-      upd[j] = j < n_out && coef_nterm(k, dj[j]) > 0;
-      accr[j] = (j == n_out - 1) ? acc_t
-                                 : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << P.n) + ((size_t)h << L), TBYTES);
-      if (ab & 16) upd[j] = false;
-      if (!LEAN && upd[j] && k > 1) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) av[j][r] = bld(accr[j], voff, (uint32_t)(r * NT * 16));
-      }
+    for (int j = 0; j < kSpanMaxOut; ++j) {
+      const int nt = j < n_out ? coef_nterm(k, dj[j], j % 3) : 0;
+      if (nt > 0 && !(ab & 16)) um |= 1u << j;
+      ntp |= (uint32_t)nt << (2 * j);
     }
+    auto acc_rsrc = [&](int j) {
+      return (j == n_out - 1) ? acc_t
+                              : tile_rsrc(P.xacc + ((size_t)(q * P.xacc_q + j) << P.n) + ((size_t)h << L), TBYTES);
+    };
+    double2 av[SL][R];
+    auto load_sums = [&](uint32_t m) {  // the first SL outputs of m
+#pragma unroll
+      for (int sl = 0; sl < SL; ++sl) {
+        if (!m) break;
+        const __amdgpu_buffer_rsrc_t ar = acc_rsrc(__builtin_ctz(m));
+        m &= m - 1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) av[sl][r] = bld(ar, voff, (uint32_t)(r * NT * 16));
+      }
+    };
+    if (!LEAN && k > 1) load_sums(um);
 
     // ---- phase 4: cross-tile operands.  Lane o of each wave polls operand o's partner flag, all
     // at once (one round trip when the partners are ahead); then the operands' rows are loaded
@@ -461,25 +474,27 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
       }
     }
     rows_lds<NT, R>(cur, tid, own);  // w_{k-1} (re-read: not held across the loop)
+    for (uint32_t m = um, first = 1; m; first = 0) {  // rounds of SL sums (one round but at rare terms)
+      if ((LEAN || !first) && k > 1) load_sums(m);
 #pragma unroll
-    for (int j = 0; j < kMaxOut; ++j) {
-      if (!upd[j]) continue;
-      if (LEAN && k > 1) {
+      for (int sl = 0; sl < SL; ++sl) {
+        if (!m) break;
+        const int j = __builtin_ctz(m);
+        m &= m - 1;
+        const int nt = (int)((ntp >> (2 * j)) & 3u);
+        const __amdgpu_buffer_rsrc_t ar = acc_rsrc(j);
+        const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);  // a_{k-2}, a_{k-1}, a_k
+        const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
+                      c1 = nt >= 2 ? make_double2(cc[2], cc[3]) : make_double2(0.0, 0.0),
+                      c2 = make_double2(cc[4], cc[5]);
 #pragma unroll
-        for (int r = 0; r < R; ++r) av[j][r] = bld(accr[j], voff, (uint32_t)(r * NT * 16));
-      }
-      const int nt = coef_nterm(k, dj[j]);
-      const auto cc = crow + j * rstride + 2 * (size_t)(k - 1);
-      const double2 c0 = nt >= 3 ? make_double2(cc[0], cc[1]) : make_double2(0.0, 0.0),
-                    c1 = nt >= 2 ? make_double2(cc[2], cc[3]) : make_double2(0.0, 0.0),
-                    c2 = make_double2(cc[4], cc[5]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        double2 a = make_double2(0.0, 0.0);
-        if (k > 1) a = cmad(av[j][r], c0.x, c0.y, prev[r]);
-        a = cmad(a, c1.x, c1.y, own[r]);
-        a = cmad(a, c2.x, c2.y, out[r]);
-        bst(accr[j], voff, (uint32_t)(r * NT * 16), a);
+        for (int r = 0; r < R; ++r) {
+          double2 a = make_double2(0.0, 0.0);
+          if (k > 1) a = cmad(av[sl][r], c0.x, c0.y, prev[r]);
+          a = cmad(a, c1.x, c1.y, own[r]);
+          a = cmad(a, c2.x, c2.y, out[r]);
+          bst(ar, voff, (uint32_t)(r * NT * 16), a);
+        }
       }
     }
 #pragma unroll
@@ -501,6 +516,8 @@ k_span(const DevProb* __restrict__ probs, const SpanDesc* __restrict__ sdesc,
 
 }  // namespace
 
+// (11, 3) -- 256 threads of 8 rows, one wave per SIMD, 102 AGPRs of spill -- measured 13.5 against
+// 11.4 us per term (lone shell_off register, profiles/r05/ab/span_rb3_256thread_dropped.jsonl)
 #define DSE_SPAN_CONFIGS(X) X(11, 2) X(10, 2) X(10, 1)
 
 bool span_supported(int L, int RB) {

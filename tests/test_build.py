@@ -97,3 +97,42 @@ def test_real_kernel_does_not_spill(tmp_path):
     kernels = [k for k in _resources(res.stderr) if "k_realILi0E" in k[0]]
     assert len(kernels) == 1, _resources(res.stderr)
     assert all(sp == 0 and sc == 0 for _, sp, sc in kernels), kernels
+
+
+def test_coef_schedule_covers_every_term_once(tmp_path):
+    """coef_nterm (dse_internal.h): for every update phase (k_span staggers output j to phase
+    j % 3) and series degree d, the terms accumulated at k = 1..d are exactly a_0..a_d, each once,
+    and no update reaches further back than w_{k-2}; phase 0 is the k_interval / k_real schedule
+    (updates at k = 1, 4, 7, ... and the remainder at k = d)."""
+    src = tmp_path / "sched.cpp"
+    src.write_text(r'''
+#include "dse_internal.h"
+#include <cstdio>
+int main() {
+  for (int ph = 0; ph < 3; ++ph)
+    for (int d = 1; d <= 400; ++d) {
+      int next = 0;  // first term not yet accumulated
+      for (int k = 1; k <= d + 1; ++k) {
+        const int n = dse::coef_nterm(k, d, ph);
+        if (k > d) { if (n) return 1; continue; }
+        if (n > 3 || (k == 1 && n != 2)) return 2;
+        if (n == 0) continue;
+        if (k - n + 1 != (k == 1 ? 0 : next) && !(k == 1 && next == 0)) return 3;
+        next = k + 1;
+      }
+      if (next != d + 1) return 4;
+      if (ph == 0)
+        for (int k = 2; k <= d; ++k)
+          if ((dse::coef_nterm(k, d, 0) == 3) != ((k - 1) % 3 == 0)) return 5;
+    }
+  std::puts("ok");
+  return 0;
+}
+''')
+    exe = tmp_path / "sched"
+    res = subprocess.run([_hipcc(), "-std=c++17", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
+                          "-x", "hip", "--offload-arch=gfx950", str(src), "-o", str(exe)],
+                         capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-2000:]
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert run.returncode == 0 and run.stdout.strip() == "ok", (run.returncode, run.stdout, run.stderr)

@@ -41,6 +41,7 @@ def _evolve(engine, probs, t, **opts):
         engine.set_option("span", 0)
         engine.set_option("span_tile", -1)
         engine.set_option("outputs_per_launch", 2)
+        engine.set_option("span_outputs", 4)
         engine.set_option("matrix", 1)
         engine.clear()
 
@@ -70,13 +71,14 @@ def test_spanned_registers_match_reference_n14(engine, golden, opt):
     print(f"N=14 spanned ({opt}): max |GPU - reference-H oracle| = {worst:.2e}")
 
 
-@pytest.mark.parametrize("m", [2, 1])
+@pytest.mark.parametrize("m", [4, 3, 2, 1])
 def test_spanned_evolve_is_repeatable(engine, m):
+    """Option span_outputs = M outputs per launch (k_span staggers output j's sum to phase j % 3)."""
     t = np.linspace(0.0, 2e-4, 21)
     probs = [pb.build_problem(_params(v, d, t)) for v in VARIANTS for d in DELTAS]
     runs = []
     for _ in range(3):
-        obs, st = _evolve(engine, probs, t, span_tile=11, outputs_per_launch=m)
+        obs, st = _evolve(engine, probs, t, span_tile=11, span_outputs=m)
         assert st["span_problems"] == 9 and st["outputs_per_launch"] == m
         runs.append(obs)
     for r in runs[1:]:
