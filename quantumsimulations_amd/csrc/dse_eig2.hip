@@ -228,6 +228,24 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
   }
 }
 
+// sum over g < ng of part[g kB^2 + e] in a fixed order: eight interleaved partial sums (g mod 8),
+// so eight loads are in flight per thread instead of one dependent add per load
+__device__ __forceinline__ double sum_partials(const double* __restrict__ part, int ng, int e) {
+  double a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.0;
+  int g = 0;
+  for (; g + 8 <= ng; g += 8) {
+    double x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = part[(size_t)(g + i) * kB * kB + e];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += x[i];
+  }
+  for (int i = 0; g + i < ng; ++i) a[i] += part[(size_t)(g + i) * kB * kB + e];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
 // T (kB x kB upper, ld kB) of the panel's block reflector I - V T V^T (LAPACK dlarft, forward,
 // columnwise): T(j, j) = tau_j, T(0:j, j) = -tau_j T(0:j, 0:j) (V^T V)(0:j, j), with V^T V the sum
 // of k_sb_vty's partials (fixed order); one workgroup
@@ -236,9 +254,7 @@ k_sb_tmat(const double* __restrict__ part, int ng, int k, const double* __restri
   __shared__ double G[kB][kB + 1];
   __shared__ double Ts[kB][kB + 1];
   const int e = threadIdx.x, p = e % kB, q = e / kB;
-  double a = 0.0;
-  for (int g = 0; g < ng; ++g) a += part[(size_t)g * kB * kB + e];
-  G[p][q] = a;
+  G[p][q] = sum_partials(part, ng, e);
   Ts[p][q] = 0.0;
   __syncthreads();
   for (int j = 0; j < k; ++j) {
@@ -424,6 +440,101 @@ k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt
     }
 }
 
+// The same update, kSyr2kNJ column tiles J per workgroup (one row block I): P = [V_I | W_I] is shared
+// by the tiles and the four waves, staged once in LDS; each lane holds rows (2 li, 2 li + 1) of
+// an output pair (the MFMAs of row halves sc = 2 sp + par take P rows 32 sp + 2 li + par), so A is
+// read and written with 16-B accesses.  Column tiles jlo .. jhi (the launch's cmin .. cmax range);
+// tiles above the diagonal idle.
+constexpr int kSyr2kNJ = 4;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256)
+k_sb_syr2k2(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt, const double* __restrict__ Wt,
+            int cmin, int cmax) {
+  constexpr int PLD = 2 * kB + 2;  // LDS row stride (doubles)
+  __shared__ __attribute__((aligned(16))) double Ps[kT][PLD];
+  const int I = blockIdx.x;
+  const int jlo = cmin / kT + (int)blockIdx.y * kSyr2kNJ;
+  const int jhi = min(min(I, (cmax - 1) / kT), jlo + kSyr2kNJ - 1);
+  if (jlo > jhi) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lq = lane >> 4;
+  const int r0 = I * kT;
+  // A22 through a buffer resource: an element outside the update (column outside cmin .. cmax, row
+  // >= m) takes an out-of-range offset (load 0, store dropped).  Elements above the diagonal inside
+  // the diagonal tiles are updated too: nothing reads A22's upper triangle (k_sb_symm and the panel
+  // QR read the lower one), so no row is a branch
+  const __amdgpu_buffer_rsrc_t ar = ptr_rsrc(A, ((size_t)(m - 1) * lda + m) * 8);
+  const __amdgpu_buffer_rsrc_t vr = ptr_rsrc(Vt, (size_t)m * kB * 8), wr = ptr_rsrc(Wt, (size_t)m * kB * 8);
+  constexpr uint32_t kOOB = 0xffffffffu;
+  for (int e = tid; e < kT * kB; e += 256) {  // 16-B pieces: row r, k pair (Vt | Wt)
+    const int r = e / kB, kk = 2 * (e % kB);
+    const uint32_t off = r0 + r < m ? (uint32_t)(((r0 + r) * kB + (kk & (kB - 1))) * 8) : kOOB;
+    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(kk < kB ? vr : wr, (int)off, 0, 0);
+    *reinterpret_cast<u32x4_t*>(&Ps[r][kk]) = v;
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int J = jlo; J <= jhi; ++J) {
+    const int c0 = J * kT;
+    // A row pairs (sp, x): rows gr, gr + 1 of column gc; a pair cut by row m (m odd) takes the
+    // single-element path
+    uint32_t aoff[2][4];
+    bool split[2][4];
+    u32x4_t old[2][4];
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int gc = c0 + 16 * w + lq + 4 * x, gr = r0 + 32 * sp + 2 * li;
+        const bool col = gc >= cmin && gc < cmax;
+        aoff[sp][x] = (col && gr + 1 < m) ? (uint32_t)(((size_t)gc * lda + gr) * 8) : kOOB;
+        split[sp][x] = col && gr + 1 == m;
+        old[sp][x] = __builtin_amdgcn_raw_buffer_load_b128(ar, (int)aoff[sp][x], 0, 0);
+        if (split[sp][x]) {
+          const u32x2_t h = __builtin_amdgcn_raw_buffer_load_b64(ar, (int)(((size_t)gc * lda + gr) * 8), 0, 0);
+          old[sp][x].x = h.x;
+          old[sp][x].y = h.y;
+        }
+      }
+    double qa[16];
+    {
+      const int qc = c0 + 16 * w + li;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t off = qc < m ? (uint32_t)((qc * kB + (u & 3) * 8 + 2 * lq) * 8) : kOOB;
+        const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(u < 4 ? wr : vr, (int)off, 0, 0);
+        const double2 d = __builtin_bit_cast(double2, v);
+        qa[2 * u] = d.x;
+        qa[2 * u + 1] = d.y;
+      }
+    }
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {  // row half sp: the two MFMA row sets par = 0, 1, then its stores
+      f64x4 acc[2];
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        const double* prow = &Ps[32 * sp + 2 * li + par][0];
+        acc[par] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double2 pb = *reinterpret_cast<const double2*>(prow + (u >> 2) * kB + (u & 3) * 8 + 2 * lq);
+          acc[par] = mfma64(qa[2 * u], pb.x, acc[par]);
+          acc[par] = mfma64(qa[2 * u + 1], pb.y, acc[par]);
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const double2 o = __builtin_bit_cast(double2, old[sp][x]);
+        const double2 nv = double2{o.x - acc[0][x], o.y - acc[1][x]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, nv), ar, (int)aoff[sp][x], 0, 0);
+        if (split[sp][x]) {
+          const int gc = c0 + 16 * w + lq + 4 * x, gr = r0 + 32 * sp + 2 * li;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, nv.x), ar, (int)(((size_t)gc * lda + gr) * 8), 0, 0);
+        }
+      }
+    }
+  }
+}
+
 // Y <- Y T (T kB x kB upper, ld kB): one thread per output Y(r, q) (32 per row, the row's Y in
 // L1), T in LDS
 __global__ void __launch_bounds__(256)
@@ -516,9 +627,7 @@ __global__ void __launch_bounds__(kB * kB)
 k_sb_gm(const double* __restrict__ part, int ng, int k, const double* __restrict__ T, double* __restrict__ Gm) {
   __shared__ double M[kB][kB];
   const int e = threadIdx.x, p = e % kB, q = e / kB;
-  double a = 0.0;
-  for (int g = 0; g < ng; ++g) a += part[(size_t)g * kB * kB + e];
-  M[p][q] = a;
+  M[p][q] = sum_partials(part, ng, e);
   __syncthreads();
   double gsum = 0.0;
   for (int i = 0; i <= p; ++i) gsum = fma(T[(size_t)p * kB + i], M[i][q], gsum);  // T^T(p, i) = T(i, p)
@@ -1263,11 +1372,12 @@ int g_q2_variant = 5;
 // default), 2 k_sb2st_pf with the next task's loads issued before the stores (280 ms: the progress
 // flag then waits for sweep s - 1 too)
 int g_chase_variant = 1;
-// the trailing update's grid: 0 2-D (nbk x nbk, the upper tiles idle; default), 1 1-D over the lower
-// tiles (band 413-425 vs 377 ms at 2^14: the 2-D order, I fastest, keeps a column's V/W rows warm)
-int g_syr2k_tri = 0;
+// the trailing update's grid: 0 2-D (nbk x nbk, the upper tiles idle), 1 1-D over the lower tiles
+// (band 413-425 vs 377 ms at 2^14: the 2-D order, I fastest, keeps a column's V/W rows warm), 2
+// k_sb_syr2k2 (P in LDS, kSyr2kNJ tiles per workgroup, 16-B row pairs; default)
+int g_syr2k_tri = 2;
 #else
-constexpr int g_q2_variant = 5, g_chase_variant = 1, g_syr2k_tri = 0;
+constexpr int g_q2_variant = 5, g_chase_variant = 1, g_syr2k_tri = 2;
 #endif
 
 struct Eig2Ws {
@@ -1392,6 +1502,20 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
                        ws.T + (size_t)p * kB * kB);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   };
+  // A22 -= V W^T + W V^T on the columns cmin .. cmax - 1
+  auto launch_syr2k = [&](double* A22, int m, const double* Vt, int cmin, int cmax) {
+    const int nbk = (m + kT - 1) / kT;
+    if (g_syr2k_tri == 2) {
+      const int nj = ((cmax - 1) / kT - cmin / kT) / kSyr2kNJ + 1;
+      hipLaunchKernelGGL(k_sb_syr2k2, dim3(nbk, nj), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, cmin, cmax);
+    } else if (g_syr2k_tri == 1) {
+      const int ntri = nbk * (nbk + 1) / 2;
+      hipLaunchKernelGGL(k_sb_syr2k, dim3(ntri), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, cmin, cmax, ntri);
+    } else {
+      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, cmax <= kB ? 1 : nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt,
+                         cmin, cmax, 0);
+    }
+  };
   int rc = 0, p = 0;
   const int last = n - kB - 1;  // panels at i < last
   if (last > 0) rc = factor(0, 0, st);
@@ -1402,7 +1526,6 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     const double* Vw = ws.Vw2[par];
     const double* Vt = ws.Vt2[par];
     const int nbk = (m + kT - 1) / kT, ng = (m + kVtyRows - 1) / kVtyRows, nch = (nbk + kSymmCh - 1) / kSymmCh;
-    const int ntri = nbk * (nbk + 1) / 2;
     if (p > 0 && hipStreamWaitEvent(st, evP, 0) != hipSuccess) rc = -1;
     double* A22 = A + (size_t)(i + kB) * lda + i + kB;
     // Y = A22 Vw T; W = Y - Vw (T^T (Vw^T Y)) / 2; A22 -= Vw W^T + W Vw^T
@@ -1413,19 +1536,13 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
     hipLaunchKernelGGL(k_sb_gm, dim3(1), dim3(kB * kB), 0, st, ws.part2, ng, k, T, ws.Gm);
     hipLaunchKernelGGL(k_sb_w, dim3((m + 63) / 64), dim3(256), 0, st, ws.Yp, Vw, m, k, ws.Gm, ws.Wt);
     if (i + kB < last) {
-      hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, 1), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, kB, 0);
+      launch_syr2k(A22, m, Vt, 0, kB);
       if (hipEventRecord(evS, st) != hipSuccess || hipStreamWaitEvent(s2, evS, 0) != hipSuccess) rc = -1;
       if (rc == 0) rc = factor(i + kB, p + 1, s2);
       if (rc == 0 && hipEventRecord(evP, s2) != hipSuccess) rc = -1;
-      if (g_syr2k_tri)
-        hipLaunchKernelGGL(k_sb_syr2k, dim3(ntri), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, kB, m, ntri);
-      else
-        hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, kB, m, 0);
+      launch_syr2k(A22, m, Vt, kB, m);
     } else {
-      if (g_syr2k_tri)
-        hipLaunchKernelGGL(k_sb_syr2k, dim3(ntri), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, m, ntri);
-      else
-        hipLaunchKernelGGL(k_sb_syr2k, dim3(nbk, nbk), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, 0, m, 0);
+      launch_syr2k(A22, m, Vt, 0, m);
     }
   }
   if (hipGetLastError() != hipSuccess && rc == 0) rc = -1;
