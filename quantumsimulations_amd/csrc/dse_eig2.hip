@@ -1169,13 +1169,16 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
       // NC = 1: the rows group t + 1 adds (lo + kQ2Win ..), loaded while group t is applied: block
       // i - 1 has stored them once its group t + 1 is flagged
       double nxt[kB];
-      if constexpr (PF) {
-        if (t + 1 < T0) {
-          wait_prev(t + 1);
+      auto prefetch_rows = [&]() {
+        if constexpr (PF) {
+          if (t + 1 < T0) {
+            wait_prev(t + 1);
 #pragma unroll
-          for (int r = 0; r < kB; ++r) nxt[r] = zld(lo + kQ2Win + r, 0);
+            for (int r = 0; r < kB; ++r) nxt[r] = zld(lo + kQ2Win + r, 0);
+          }
         }
-      }
+      };
+      if constexpr (!DMA) prefetch_rows();
       const double* rg = rv;  // this group's records
       if constexpr (SC) {
         const uint64_t ga = (uint64_t)(gb + (size_t)t * kQ2Rec);
@@ -1187,6 +1190,7 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
         __builtin_amdgcn_wave_barrier();
         rg = rv + (t & 1) * kQ2Dma * 128;
         if (t + 1 < T0) dma(t + 1);
+        prefetch_rows();  // after the wait: the next rows load under this group
       } else {
 #pragma unroll
         for (int q = 0; q < kQ2PerLane; ++q) rv[q * 64 + lane] = pre[q];
@@ -1366,7 +1370,8 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
 // reflector at a time, rows loaded after each group (346 ms); 1 pairs + the next rows under the
 // group (361); 2 two columns per lane (649); 3 pairs (357); 4 = 0 with the records copied global ->
 // LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default); 6 / 7 the reflector values
-// as scalar-load SGPR operands, 8 / 4 waves (512 / 921: each reflector waits on its s_loads)
+// as scalar-load SGPR operands, 8 / 4 waves (512 / 921: each reflector waits on its s_loads); 8 =
+// 5 with the next rows loaded under the group (354 vs 296 ms, round 5: 25 VGPRs of spill)
 int g_q2_variant = 5;
 // the chase: 0 k_sb2st (waits for (s - 1, t + 2) complete: 336 ms at 2^14), 1 k_sb2st_pf (243 ms,
 // default), 2 k_sb2st_pf with the next task's loads issued before the stores (280 ms: the progress
@@ -1613,6 +1618,7 @@ int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
     case 5: hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 8>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 6: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 8, true>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 7: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4, true>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 8: hipLaunchKernelGGL((k_sb_q2<1, true, false, true, 8>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     default: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
   }
 #endif

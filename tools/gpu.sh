@@ -12,6 +12,7 @@
 #   traffic                    FETCH_SIZE and WRITE_SIZE passes of the same (one counter per run)
 #   traffic_large              the same over tools/bench_large.py (N = 30, Walsh-Hadamard engine)
 #   sq:<set>                   three SQ counter passes over tools/probe_one.py <set>
+#   sqeig:<dim>                the same over tools/bin/probe_eig2 <dim>
 #   sytrd:<dim,...>            tools/bin/probe_sytrd <dim> check
 #   eig2:<dim[/random],...>    tools/bin/probe_eig2 (two-stage eigensolver vs dsyevd)
 #   py:<script>,<args...>      python -u <script> <args> > <tag>/<script-name>.out
@@ -58,8 +59,9 @@ for T in "$@"; do
       [ $rc -eq 0 ] || fail fetch_large
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/large/write -o write --output-format csv -- python3 tools/bench_large.py --steps 3 > $OUT/large_write.json 2> $OUT/large_write.err; rc=$?
       [ $rc -eq 0 ] || fail write_large ;;
-    sq)
+    sq|sqeig)  # sqeig:<dim>: the same passes over tools/bin/probe_eig2 <dim>
       PMC_CMD=(python3 tools/probe_one.py "${A[@]}"); q=$(echo "${A[*]}" | tr ' =' '__')_
+      [ $task = sqeig ] && PMC_CMD=(tools/bin/probe_eig2 "${A[@]}") && q=eig2_${q}
       pmc ${q}p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU; rc=$?
       [ $rc -eq 0 ] || fail sq p1
       pmc ${q}p2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE; rc=$?
