@@ -1100,7 +1100,7 @@ constexpr int kQ2PerLane = (kQ2Rec + 63) / 64;    // staging loads per lane
 constexpr int kQ2Dma = (kQ2Rec * 8 + 1023) / 1024;  // 1-KiB copies per group
 // SC: the reflector values are read with scalar loads straight from the records (uniform across the
 // wave: SGPR operands of the FMAs, no LDS traffic); the records are written by earlier launches.
-template <int NC, bool PF, bool PAIR, bool DMA, int W, bool SC = false>
+template <int NC, bool PF, bool PAIR, bool DMA, int W, bool SC = false, bool NL = false>
 __global__ void __launch_bounds__(64 * W)
 k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl, const long long* __restrict__ goff) {
   constexpr int kBuf = SC ? 2 : DMA ? 2 * kQ2Dma * 128 : kQ2PerLane * 64;  // doubles per wave
@@ -1313,10 +1313,12 @@ k_sb_q2(double* __restrict__ Zt, int ldt, int n, const double* __restrict__ refl
           for (int r = 0; r < kB; ++r) win[0][kQ2Win - kB + r] = nxt[r];
         } else {
           wait_prev(t + 1);
+          if constexpr (!NL) {  // NL (probe ablation only, wrong results): the new rows not loaded
 #pragma unroll
-          for (int c = 0; c < NC; ++c)
+            for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int r = 0; r < kB; ++r) win[c][kQ2Win - kB + r] = zld(lo + kQ2Win + r, c);
+              for (int r = 0; r < kB; ++r) win[c][kQ2Win - kB + r] = zld(lo + kQ2Win + r, c);
+          }
         }
         lo += kB;
       }
@@ -1371,7 +1373,11 @@ k_sb_transpose(const double* __restrict__ A, int lda, double* __restrict__ B, in
 // group (361); 2 two columns per lane (649); 3 pairs (357); 4 = 0 with the records copied global ->
 // LDS (371); 5 = 4 with 8 waves per workgroup, 2 per SIMD (296, default); 6 / 7 the reflector values
 // as scalar-load SGPR operands, 8 / 4 waves (512 / 921: each reflector waits on its s_loads); 8 =
-// 5 with the next rows loaded under the group (354 vs 296 ms, round 5: 25 VGPRs of spill)
+// 5 with the next rows loaded under the group (354 vs 296 ms, round 5: 25 VGPRs of spill; issued
+// late in the group the same, 378 ms); 9 = 5 without the new window rows (ablation, wrong results:
+// 249 ms, so their exposed load is ~47 ms).  Round 5 also measured the update pass re-reading the
+// reflector from LDS instead of holding it (405 ms; with the prefetch 432): the broadcast LDS reads
+// are part of the bound (profiles/r05/ab/eig2_q2_variants_r05.txt)
 int g_q2_variant = 5;
 // the chase: 0 k_sb2st (waits for (s - 1, t + 2) complete: 336 ms at 2^14), 1 k_sb2st_pf (243 ms,
 // default), 2 k_sb2st_pf with the next task's loads issued before the stores (280 ms: the progress
@@ -1619,6 +1625,7 @@ int q2_apply(hipStream_t st, int n, double* Z, int ldz, void* work) {
     case 6: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 8, true>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 7: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4, true>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     case 8: hipLaunchKernelGGL((k_sb_q2<1, true, false, true, 8>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
+    case 9: hipLaunchKernelGGL((k_sb_q2<1, false, false, true, 8, false, true>), g1, dim3(512), 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
     default: hipLaunchKernelGGL((k_sb_q2<1, false, false, false, 4>), g1, blk, 0, st, ws.Zt, n, n, ws.refl, ws.goff); break;
   }
 #endif
