@@ -209,8 +209,9 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         cooperating workgroups, one per CU, with per-term cross-tile hand-offs
  *                         (k_span, dse_span.hip): a shorter chain per register for few registers
  *                         (one simulate_rare call, one GPU's share of a strong split); -1
- *                         (default): L = 11 when every Chebyshev register of the evolve is 12..15
- *                         qubits and all their tiles fit the chip at once, else none; 0 never
+ *                         (default): when every Chebyshev register of the evolve is 12..15 qubits,
+ *                         L = 10 if all their tiles fit one per CU, else L = 11 if they fit the
+ *                         chip at once, else none; 0 never
  *          "span"         the same with a fixed number s = 1..4 of top bits per register
  *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
  *          "span_outputs" outputs per launch (1..4, default 4) of an evolve whose registers all

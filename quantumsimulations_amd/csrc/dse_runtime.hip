@@ -2536,7 +2536,10 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
 
 // ---- spanning registers (dse_span.hip) ------------------------------------------------------
 
-constexpr int kSpanAutoTile = 11;  // option span_tile = -1: the tile of the automatic choice
+// option span_tile = -1: the automatic choice takes the smallest of these tiles whose workgroups
+// all fit the chip at once -- 2^10 (a lone N = 14 register over 16 CUs: 78 vs 85 ms at 150 kHz)
+// one per CU, else 2^11 at the kernel's occupancy (one GPU's share of a strong split)
+constexpr int kSpanAutoTiles[2] = {10, 11};
 
 // amplitudes per thread of k_span for an L-bit tile: 2^rb (option span_rb, else 512 threads)
 int span_rb_for(const dse_ctx* ctx, int L) { return ctx->span_rb > 0 ? ctx->span_rb : L - 9; }
@@ -2757,18 +2760,20 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     int tile = ctx->span_tile;
     if (tile < 0) {
       tile = 0;
-      int64_t wg = 0;
-      bool all = persistent && ctx->span == 0;
-      for (auto& P : ctx->probs) {
-        if (P.side()) continue;
-        const int s = P.n_local - kSpanAutoTile;
-        if (!span_eligible(ctx, P, s)) all = false;
-        wg += int64_t(1) << std::max(0, s);
+      for (int ti = 0; ti < 2 && tile == 0; ++ti) {
+        const int L = kSpanAutoTiles[ti];
+        int64_t wg = 0;
+        bool all = persistent && ctx->span == 0;
+        for (auto& P : ctx->probs) {
+          if (P.side()) continue;
+          const int s = P.n_local - L;
+          if (!span_eligible(ctx, P, s)) all = false;
+          wg += int64_t(1) << std::max(0, s);
+        }
+        int per_cu = 1;
+        if (ti > 0 && span_occupancy(L, span_rb_for(ctx, L), true, &per_cu) != hipSuccess) per_cu = 0;
+        if (all && wg > 0 && wg <= (int64_t)per_cu * ctx->n_cu) tile = L;
       }
-      int per_cu = 1;
-      if (all && wg > 0 && span_occupancy(kSpanAutoTile, span_rb_for(ctx, kSpanAutoTile), true, &per_cu) == hipSuccess &&
-          wg <= (int64_t)std::max(1, per_cu) * ctx->n_cu)
-        tile = kSpanAutoTile;
     }
     for (auto& P : ctx->probs) {
       const int s = tile > 0 ? P.n_local - tile : ctx->span;
