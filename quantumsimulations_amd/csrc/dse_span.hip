@@ -66,8 +66,8 @@ struct SpanGeo {
   static constexpr int IW = 4 + NPI;                   // dv2 per iteration row
   static constexpr uint32_t TBYTES = (16u << L);
   // u operands built per pre-pass sweep (2^11-amplitude tiles have at most 3 top bits at n <= 14,
-  // and 3 keeps the pipelined pre-pass inside the register budget there)
-  static constexpr int US = (R <= 4 && NT < 1024) ? (TB >= 9 ? 3 : 4) : 2;
+  // and 3 keeps the pipelined pre-pass inside the register budget there; 2-row threads hold 4)
+  static constexpr int US = R <= 2 ? 4 : (R <= 4 && NT < 1024) ? (TB >= 9 ? 3 : 4) : 2;
 };
 
 template <bool IMAG>
