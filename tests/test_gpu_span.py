@@ -109,3 +109,17 @@ def test_automatic_span_policy(engine):
     off, st_o = _evolve(engine, probs, t, span_tile=0)
     assert st_a["span_problems"] == 9 and st_o["span_problems"] == 0
     assert float(np.max(np.abs(auto - off))) < 1e-11
+
+
+def test_output_count_options_are_range_checked(engine):
+    """span_outputs takes 1..4 (k_span staggers the sums); outputs_per_launch stays 1..2 (k_interval
+    and k_real hold the sums of one term in registers); a bad value is refused, the old one kept."""
+    for key, bad in (("span_outputs", 5), ("span_outputs", 0), ("outputs_per_launch", 3)):
+        with pytest.raises(ValueError):
+            engine.set_option(key, bad)
+    t = np.linspace(0.0, 1e-4, 11)
+    probs = [pb.build_problem(_params("center_on", 75000, t))]
+    _, st = _evolve(engine, probs, t, span_tile=11)
+    assert st["span_problems"] == 1 and st["outputs_per_launch"] == 4
+    _, st = _evolve(engine, probs, t, span_tile=0)
+    assert st["span_problems"] == 0 and st["outputs_per_launch"] == 2
