@@ -92,8 +92,6 @@ __device__ __forceinline__ void rd_pairs(uint32_t wbase, int tp, int hh, int pp0
 // stores, 16 the w_k stores
 #ifdef DSE_DIAG
 int g_real_ablate = 0;
-#else
-constexpr int g_real_ablate = 0;
 #endif
 
 template <int L, int ABL>
