@@ -37,7 +37,10 @@ namespace {
 
 constexpr int kB = 32;              // bandwidth of stage 1 = reflector length of stage 2
 constexpr int kLD = 2 * kB + 2;     // band storage per column: d = 0 .. 2b, one pad
-constexpr int kPanelRows = 256;     // panel QR: rows (threads) per workgroup
+// panel QR: rows (threads) per workgroup.  512 against 256: half the workgroups whose partial sums
+// every column's exchange gathers, band stage 312 -> 300 ms at 2^14; 1024 spills (329 ms)
+// (profiles/r05/ab/panel_qr_rows_ab.txt)
+constexpr int kPanelRows = 512;
 constexpr int kQ2NB = 32;           // Q2 application: sweeps per group
 constexpr int kQ2Win = kQ2NB + kB;  // window rows per column
 
@@ -99,8 +102,9 @@ __global__ void __launch_bounds__(kPanelRows)
 k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, double* __restrict__ part,
            double* __restrict__ piv, double* __restrict__ Vw, double* __restrict__ Vt, int* __restrict__ err,
            int spin) {
-  __shared__ double red[kPanelRows / 64][kB];
-  __shared__ double red8[8][kB];
+  constexpr int NW = kPanelRows / 64, NG0 = kPanelRows / 32, NQ = 128 / NG0;  // waves; partial sums
+  __shared__ double red[NW][kB];
+  __shared__ double red8[NG0][kB];
   __shared__ double tot[kB];
   __shared__ double prow[kB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -146,29 +150,34 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
         if (k >= j) bstore(vrs, j * kB + k, x[k]);
     }
     __syncthreads();
-    if (tid < kB && tid >= j) bstore(prs, pj + tid, red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
-    {  // the G partials: thread (k, g0) sums g = g0, g0 + 8, ... (G <= 128), then the 8 in fixed order
-      const int k = tid & 31, g0 = tid >> 5;
-      double pv[16];
-      auto slot = [&](int q) { return (j * G + g0 + 8 * q) * (kB + 1) + k; };
-      auto live = [&](int q) { return k >= j && g0 + 8 * q < G; };
+    if (tid < kB && tid >= j) {
+      double a = 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pv[q] = live(q) ? bload(prs, slot(q)) : 0.0;
+      for (int w = 0; w < NW; ++w) a += red[w][tid];
+      bstore(prs, pj + tid, a);
+    }
+    {  // the G partials: thread (k, g0) sums g = g0, g0 + NG0, ... (G <= 128), then the NG0 in fixed order
+      const int k = tid & 31, g0 = tid >> 5;
+      double pv[NQ];
+      auto slot = [&](int q) { return (j * G + g0 + NG0 * q) * (kB + 1) + k; };
+      auto live = [&](int q) { return k >= j && g0 + NG0 * q < G; };
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) pv[q] = live(q) ? bload(prs, slot(q)) : 0.0;
       double pr = tid < kB && tid >= j ? bload(vrs, j * kB + tid) : 0.0;
       for (int it = 0;; ++it) {
         bool miss = is_sentinel(pr);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) miss |= is_sentinel(pv[q]);
+        for (int q = 0; q < NQ; ++q) miss |= is_sentinel(pv[q]);
         if (!miss || poll_give_up(err, spin, it)) break;
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
+        for (int q = 0; q < NQ; ++q)
           if (is_sentinel(pv[q])) pv[q] = bload(prs, slot(q));
         if (is_sentinel(pr)) pr = bload(vrs, j * kB + tid);
       }
       double s = 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) s += pv[q];
+      for (int q = 0; q < NQ; ++q) s += pv[q];
       red8[g0][k] = s;
       if (tid < kB) prow[tid] = pr;
     }
@@ -176,7 +185,7 @@ k_panel_qr(double* __restrict__ P, int lda, int m, double* __restrict__ tau, dou
     if (tid < kB) {
       double s = 0.0;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) s += red8[g][tid];
+      for (int g = 0; g < NG0; ++g) s += red8[g][tid];
       tot[tid] = s;
     }
     __syncthreads();
