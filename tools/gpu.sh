@@ -4,7 +4,7 @@
 #   tools/gpu.sh <tag> <task>[:arg,arg...] [<task>...]
 #
 # Every task runs under its own time limit; the first failure ends the call (no GPU step after
-# a fault, an abort or a time limit).  Outputs land in gpurun_out/r05/<tag>/.
+# a fault, an abort or a time limit).  Outputs land in gpurun_out/r06/<tag>/.
 #   tests[:pytest-path-or-k]   pytest -m gpu (whole suite, a file, or "-k expr" as k=expr)
 #   smoke                      __graft_entry__.smoke()
 #   bench[:args]               python bench.py <args>  (args: comma-separated)
@@ -18,7 +18,7 @@
 #   py:<script>,<args...>      python -u <script> <args> > <tag>/<script-name>.out
 set -o pipefail
 TAG=${1:?tag}; shift
-OUT=gpurun_out/r05/$TAG
+OUT=gpurun_out/r06/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 LEGS="--no-cpu-baseline --no-large --no-full --no-config2 --no-refdefault"
@@ -44,7 +44,7 @@ for T in "$@"; do
       cat $OUT/smoke.log; [ $rc -eq 0 ] || fail smoke ;;
     bench)
       nb=$((nb + 1)); b=$OUT/bench$([ $nb -gt 1 ] && echo _$nb)
-      timeout -k 10 900 python -u bench.py "${A[@]}" > $b.json 2> $b.err; rc=$?
+      DSE_BENCH_DETAIL=$b.detail.json timeout -k 10 900 python -u bench.py "${A[@]}" > $b.json 2> $b.err; rc=$?
       head -c 600 $b.json; echo; [ $rc -eq 0 ] || { tail -5 $b.err; fail bench; } ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py $LEGS "${A[@]}" > $OUT/bench_under_rocprof.json 2> $OUT/trace.err; rc=$?

@@ -3,6 +3,8 @@
 //         quantumsimulations_amd/csrc/dse_eig2.hip quantumsimulations_amd/csrc/dse_sytrd.hip \
 //         -lrocsolver -lrocblas -o tools/bin/probe_eig2
 //   probe_eig2 <dim> [random]
+// Exit codes: 0 ok; 2 HIP error; 3 band reduction error; 4 a bounded poll gave up (band void, the
+// later stages are not run); 5 dstedc info != 0; 6 / 7 Q2 / Q1 error.
 // Matrix: tools/probe_sytrd.cpp's (spectrum and sparsity of the N = 14 rotated H') or, with
 // "random", a dense symmetric one.  One JSON line per stage timing, then the check: max |lam -
 // lam_dsyevd| / max |lam|, max |A V - V diag(lam)| / max |lam|, max |V^T V - I|.
@@ -123,18 +125,47 @@ int main(int argc, char** argv) {
     int rc1 = dse::sy2sb_lower(h, st, n, A, n, work);
     CK(hipStreamSynchronize(st));
     t[1] = now_ms();
+    if (rc1 != 0) {  // a launch or argument error of the band reduction: nothing after it is valid
+      std::fprintf(stderr, "sy2sb_lower rc %d: stopping before the chase\n", rc1);
+      return 3;
+    }
     int rc2 = dse::sb2st_lower(st, n, A, n, lam, e, work, n_cu, dse::kEig2DefaultSpin, dbg);
     CK(hipStreamSynchronize(st));
     t[2] = now_ms();
+    if (rc2 != 0) {
+      // kEig2PollTimeout: a bounded cross-workgroup poll of the panel QR or of the chase gave up (the
+      // error word sy2sb_lower and sb2st_lower share), so the band / tridiagonal is void.  Round 5
+      // ran dstedc, Q2 and Q1 on such a void band under rocprofv3 --pmc and ended in a host SIGSEGV;
+      // stop here instead (libdse.so's dense engine re-solves such a register with dsyevd).
+      std::printf("{\"dim\": %d, \"rep\": %d, \"sy2sb_ms\": %.1f, \"sb2st_ms\": %.1f, \"rc\": [%d, %d], "
+                  "\"poll_gave_up\": %d}\n", n, rep, t[1] - t[0], t[2] - t[1], rc1, rc2,
+                  rc2 == dse::kEig2PollTimeout);
+      std::fflush(stdout);
+      return 4;
+    }
     rocsolver_dstedc(h, rocblas_evect_tridiagonal, n, lam, e, V, n, info);
     CK(hipStreamSynchronize(st));
     t[3] = now_ms();
+    rocblas_int hinfo = 0;
+    CK(hipMemcpy(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost));
+    if (hinfo != 0) {
+      std::fprintf(stderr, "dstedc info %d: stopping before Q2\n", (int)hinfo);
+      return 5;
+    }
     int rc3 = dse::q2_apply(st, n, V, n, work);
     CK(hipStreamSynchronize(st));
     t[4] = now_ms();
     // Q1 via the public two-stage entry's last step: ormtr_lower(offset 32) on the stage-1 reflectors
+    if (rc3 != 0) {
+      std::fprintf(stderr, "q2_apply rc %d: stopping before Q1\n", rc3);
+      return 6;
+    }
     int rc4 = dse::eig2_q1(h, st, n, A, n, V, n, work);
     CK(hipStreamSynchronize(st));
+    if (rc4 != 0) {
+      std::fprintf(stderr, "eig2_q1 rc %d\n", rc4);
+      return 7;
+    }
     t[5] = now_ms();
     std::printf("{\"dim\": %d, \"rep\": %d, \"sy2sb_ms\": %.1f, \"sb2st_ms\": %.1f, \"stedc_ms\": %.1f, \"q2_ms\": %.1f, "
                 "\"q1_ms\": %.1f, \"total_ms\": %.1f, \"rc\": [%d, %d, %d, %d]}\n",
