@@ -200,7 +200,8 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         0 (default): the complex kernels (k_real measured at the 2-tile
  *                         k_interval's CU cost: slower on the bench's mix, 1 and 2 alike)
  *          "spin_limit"   persistent kernels: polls of a partner workgroup's flag before a
- *                         cross-tile hand-off is declared failed (default 2^22, ~0.3 s; the call
+ *                         cross-tile hand-off is declared failed (default 2^22 poll rounds, each an s_sleep 1 and
+ *                         one flag load, so its wall time is set by that load's latency; the call
  *                         then re-runs on the streaming kernels, stats handoff_fallbacks);
  *                         -1: every hand-off fails at once (tests)
  *          "ablate", "span_ablate", "real_ablate"  diagnostics builds only (-DDSE_DIAG): skip
@@ -218,7 +219,8 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         span: k_span staggers the outputs' sums over the terms, so more
  *                         outputs per Chebyshev series cost no extra registers
  *          "eig_spin_limit"  two-stage eigensolver: rounds a poll of another workgroup's result
- *                         waits before it gives up (default 2^22, ~0.1 s); a give-up voids that
+ *                         waits before it gives up (default 2^22 poll rounds, each one buffer load of the
+ *                         polled value; counted in rounds, not time, as spin_limit); a give-up voids that
  *                         solve and the register is re-solved by rocSOLVER dsyevd (stats
  *                         eig_fallbacks); -1: every solve gives up at once (tests)
  *          "dense_refine" dense engine: 1 (default) eigenvalues refined by double-double

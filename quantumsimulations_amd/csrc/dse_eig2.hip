@@ -453,7 +453,11 @@ k_sb_syr2k(double* __restrict__ A, int lda, int m, const double* __restrict__ Vt
 // by the tiles and the four waves, staged once in LDS; each lane holds rows (2 li, 2 li + 1) of
 // an output pair (the MFMAs of row halves sc = 2 sp + par take P rows 32 sp + 2 li + par), so A is
 // read and written with 16-B accesses.  Column tiles jlo .. jhi (the launch's cmin .. cmax range);
-// tiles above the diagonal idle.
+// tiles above the diagonal idle.  A's offsets are 32-bit buffer offsets from A22 (and the buffer
+// descriptor's size is 32-bit): valid while lda * m * 8 < 2^32, which every dense register
+// (n <= kDenseMaxQubits = 14: 2^31 bytes) meets; sy2sb_lower takes k_sb_syr2k (64-bit pointer
+// arithmetic) for anything larger.
+static_assert(kDenseMaxQubits <= 14, "k_sb_syr2k2: 32-bit offsets into a 2^n x 2^n matrix");
 constexpr int kSyr2kNJ = 4;
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256)
@@ -1522,10 +1526,12 @@ int sy2sb_lower(rocblas_handle h, hipStream_t st, int n, double* A, int lda, voi
                        ws.T + (size_t)p * kB * kB);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   };
-  // A22 -= V W^T + W V^T on the columns cmin .. cmax - 1
+  // A22 -= V W^T + W V^T on the columns cmin .. cmax - 1 (k_sb_syr2k2 addresses A22 with 32-bit
+  // buffer offsets: only while the whole matrix spans < 4 GiB)
+  const bool wide_ok = (size_t)n * (size_t)lda * 8u < ((size_t)1 << 32);
   auto launch_syr2k = [&](double* A22, int m, const double* Vt, int cmin, int cmax) {
     const int nbk = (m + kT - 1) / kT;
-    if (g_syr2k_tri == 2) {
+    if (g_syr2k_tri == 2 && wide_ok) {
       const int nj = ((cmax - 1) / kT - cmin / kT) / kSyr2kNJ + 1;
       hipLaunchKernelGGL(k_sb_syr2k2, dim3(nbk, nj), dim3(256), 0, st, A22, lda, m, Vt, ws.Wt, cmin, cmax);
     } else if (g_syr2k_tri == 1) {

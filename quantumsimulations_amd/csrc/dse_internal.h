@@ -150,7 +150,7 @@ struct alignas(16) SpanTab {
 // (kernel arguments: distinct contexts on one process stay independent)
 struct HandoffKnobs {
   int spin_limit = 1 << 22;  // polls of a partner's flag before the hand-off is declared failed
-                             // (s_sleep 1 between polls, ~0.3 s); < 0: every wait fails at once
+                             // (s_sleep 1 between polls; rounds, not time: include/dse.h); < 0: every wait fails at once
                              // (tests: exercises the fallback to the streaming kernels)
   int fences = 0;            // k_interval: 1 adds an agent release / acquire around each flag
 };

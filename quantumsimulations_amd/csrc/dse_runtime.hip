@@ -2106,8 +2106,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     std::vector<hipError_t> werr(K, hipSuccess);
     std::mutex qm;
     std::condition_variable qcv;
-    std::deque<Task> ready;
-    std::map<DenseJob*, int> pending;  // per job (dense_early 0): its registers not yet solved
+    std::deque<DenseJob*> ready;        // jobs whose registers are all solved: their outputs next
+    std::map<DenseJob*, int> pending;  // per job: its registers not yet solved
     for (const Task& T : tasks) pending[T.j] += 1;
     int workers_left = K;
     auto e1 = e0;
@@ -2154,7 +2154,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
         }
         std::lock_guard<std::mutex> lk(qm);
         if (--pending[&J] == 0) {
-          ready.push_back(Task{&J, -1});  // the whole job
+          ready.push_back(&J);
           qcv.notify_one();
         }
       }
@@ -2162,9 +2162,8 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       if (--workers_left == 0) e1 = std::chrono::steady_clock::now();
       qcv.notify_one();
     };
-    auto outputs = [&](const Task& T) -> int {  // registers [i0, i0 + cnt) of job T.j
-      DenseJob& J = *T.j;
-      const int i0 = T.i >= 0 ? T.i : 0, cnt = T.i >= 0 ? 1 : J.cnt, TB = J.TB;
+    auto outputs = [&](DenseJob& J) -> int {  // every register of job J
+      const int i0 = 0, cnt = J.cnt, TB = J.TB;
       const size_t dim = J.dim, pstride = J.pstride;
       const DenseProb* desc = J.d_desc + i0;
       double* const V = J.V + dim * dim * i0;
@@ -2208,15 +2207,15 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
     size_t done = 0;
     const size_t n_out_tasks = jobs.size();
     while (done < n_out_tasks) {
-      Task T{nullptr, 0};
+      DenseJob* J = nullptr;
       {
         std::unique_lock<std::mutex> lk(qm);
         qcv.wait(lk, [&] { return !ready.empty() || workers_left == 0; });
         if (ready.empty()) break;  // the workers stopped early: an error below
-        T = ready.front();
+        J = ready.front();
         ready.pop_front();
       }
-      orc = outputs(T);
+      orc = outputs(*J);
       if (orc != DSE_OK) {
         abort_all = true;
         break;
@@ -3492,9 +3491,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       for (auto& g : ln.groups) {
         const int T = 1 << g.L;
         if (persistent) {
-          // all K terms of the interval in one launch; 2-tile groups in co-resident chunks
-          // spanning registers: one k_span launch for the group (every register's tiles resident
-          // together: the runtime sizes span groups to the chip), flags zeroed first
+          // all K terms of the interval in one launch; 2-tile groups in co-resident chunks;
+          // spanning registers: one k_span launch per chunk of span_cuts (each chunk's registers'
+          // tiles all resident at once: the cuts are sized to the chip's resident capacity), flags
+          // zeroed first
           if (g.tiles < 0) HIPC(hipMemsetAsync(ctx->d_span_flags, 0, ctx->span_flag_cap, ln.stream));
           else if (g.tiles != 1) HIPC(zero_flags(ctx->d_items + g.off, (int)g.count, ctx->d_flags, ln.stream));
           auto launch_g = [&](int64_t off, int cnt) -> hipError_t {

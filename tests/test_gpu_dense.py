@@ -283,3 +283,24 @@ def test_two_stage_poll_give_up_falls_back_to_dsyevd(engine):
     assert np.max(np.abs(s_fb[0] - s_ev[0])) < 1e-11
     again, st_again, _ = _evolve(engine, [p], t, 2, eig_impl=3)   # the context is fine afterwards
     assert st_again["eig_fallbacks"] == 0 and np.array_equal(again, ok)
+
+
+@pytest.mark.parametrize("n_sea", [12, 13])
+def test_two_stage_give_up_falls_back_to_dsyevd_at_production_sizes(engine, n_sea):
+    """The sizes the default eig_impl (1) sends to the two-stage solver in production: 2^13 and 2^14
+    (n_sea = 12, 13, center_on).  eig_spin_limit = -1 makes every bounded poll give up; the dense
+    engine then re-solves with dsyevd, whose 2^14 handle workspace (~4 GiB) must fit beside the
+    dense budget.  The result is dsyevd's own (1e-11) and the fallback is counted."""
+    t = np.linspace(0.0, 2e-3, 51)
+    p = sweep_point_params(n_sea, 100e3, "center_on", 2e-3, 51)
+    engine.set_option("eig_spin_limit", -1)
+    try:
+        fb, st_fb, s_fb = _evolve(engine, [p], t, 2, eig_impl=1)
+    finally:
+        engine.set_option("eig_spin_limit", 1 << 22)
+    ev, st_ev, s_ev = _evolve(engine, [p], t, 2, eig_impl=0)
+    assert st_fb["dense_problems"] == 1 and st_fb["eig_fallbacks"] == 1
+    assert st_ev["eig_fallbacks"] == 0
+    assert np.all(np.isfinite(fb))
+    np.testing.assert_allclose(fb, ev, rtol=0, atol=1e-11)
+    assert np.max(np.abs(s_fb[0] - s_ev[0])) < 1e-11

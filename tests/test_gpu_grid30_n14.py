@@ -93,8 +93,12 @@ def test_dense_30s_n14_matches_oracle(engine, golden):
         "max_unreduced_vs_tables": float(et.max()), "at_30s_unreduced_vs_tables": float(et[-1]),
         "max_bench_registers_vs_ref": float(eb_r.max()), "max_bench_registers_vs_tables": float(eb_t.max()),
         "fixtures_ref_vs_tables": fx, "eig_fallbacks": st.get("eig_fallbacks")})
-    assert np.all(et <= TOL_NORTH_STAR), et
-    assert np.all(eb_r <= TOL_NORTH_STAR), eb_r
+    # north_star's 1e-8 and, below it, the early-time floor 1e-10 + 1.5 eps ||H|| t (refined
+    # eigenvalues: nothing may grow with t; measured 2.5e-11 over the whole grid)
+    hnorm = max(max(abs(a) for a in pb.spectral_bounds(p)) for p in _probs(False))
+    bound = np.minimum(TOL_NORTH_STAR, 1e-10 + 1.5 * np.finfo(float).eps * hnorm * t)
+    assert np.all(et <= bound), (et, bound)
+    assert np.all(eb_r <= TOL_NORTH_STAR), eb_r   # the fixtures' own 4.5e-9 difference included
 
 
 def test_chebyshev_30s_n14_prefix_against_oracle(engine, golden):
@@ -110,11 +114,14 @@ def test_chebyshev_30s_n14_prefix_against_oracle(engine, golden):
             e = np.maximum(e, np.abs(ch[i, j, idx[sel]] - g[f"tables_{v}_{DELTA}_{k}"][sel]))
     tk = T[idx[sel]]
     hnorm = max(max(abs(a) for a in pb.spectral_bounds(p)) for p in probs)
-    rate = float(np.max(e / tk))
+    # drift rate for the extrapolation to 30 s: least squares through the origin, and the envelope
+    # past the first 10 ms (earlier outputs carry the per-interval truncation floor, not the drift)
+    rate_ls = float(np.sum(e * tk) / np.sum(tk * tk))
+    rate = float(np.max((e / tk)[tk >= 0.01]))
     print(f"N=14 Chebyshev vs oracle over the first 100 intervals: {', '.join(f'{x:.1e}' for x in e)} at "
-          f"t = {', '.join(f'{x:.3f}' for x in tk)} s; envelope rate {rate:.2e}/s (eps ||H|| = "
+          f"t = {', '.join(f'{x:.3f}' for x in tk)} s; rate LS {rate_ls:.2e}/s, envelope past 10 ms {rate:.2e}/s (eps ||H|| = "
           f"{np.finfo(float).eps * hnorm:.2e}/s)")
     _record("grid30_n14_oracle_chebyshev.json", {
         "t": tk.tolist(), "t_index": idx[sel].tolist(), "err_vs_tables": e.tolist(),
-        "rate_envelope_per_s": rate, "hnorm_bound": hnorm, "eps_hnorm_per_s": float(np.finfo(float).eps * hnorm)})
+        "rate_envelope_per_s": rate, "rate_ls_per_s": rate_ls, "hnorm_bound": hnorm, "eps_hnorm_per_s": float(np.finfo(float).eps * hnorm)})
     assert np.all(e <= 1e-10 + 1.5 * np.finfo(float).eps * hnorm * tk), e

@@ -12,7 +12,7 @@
 #   traffic                    FETCH_SIZE and WRITE_SIZE passes of the same (one counter per run)
 #   traffic_large              the same over tools/bench_large.py (N = 30, Walsh-Hadamard engine)
 #   sq:<set>                   three SQ counter passes over tools/probe_one.py <set>
-#   sqeig:<dim>                the same over tools/bin/probe_eig2 <dim>
+#   sqeig:<dim>                the same over tools/bin/probe_eig2 <dim> (PMC_FILTER: a kernel regex)
 #   sytrd:<dim,...>            tools/bin/probe_sytrd <dim> check
 #   eig2:<dim[/random],...>    tools/bin/probe_eig2 (two-stage eigensolver vs dsyevd)
 #   py:<script>,<args...>      python -u <script> <args> > <tag>/<script-name>.out
@@ -26,7 +26,7 @@ step() { echo "[$(date +%T)] $*"; }
 fail() { echo "FAILED: $* (rc $rc)"; exit 1; }
 pmc() {  # name counters...
   local name=$1; shift
-  timeout -s KILL 90 rocprofv3 --pmc "$@" -d $OUT/pmc/$name -o $name --output-format csv -- "${PMC_CMD[@]}" > $OUT/pmc.$name.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc "$@" ${PMC_FILTER:+--kernel-include-regex "$PMC_FILTER"} -d $OUT/pmc/$name -o $name --output-format csv -- "${PMC_CMD[@]}" > $OUT/pmc.$name.log 2>&1
 }
 for T in "$@"; do
   task=${T%%:*}; arg=""; [ "$task" != "$T" ] && arg=${T#*:}
