@@ -212,7 +212,8 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         (one simulate_rare call, one GPU's share of a strong split); -1
  *                         (default): when every Chebyshev register of the evolve is 12..15 qubits,
  *                         L = 10 if all their tiles fit one per CU, else L = 11 if they fit the
- *                         chip at once, else none; 0 never
+ *                         chip at once or in two resident launches per interval, else none;
+ *                         0 never
  *          "span"         the same with a fixed number s = 1..4 of top bits per register
  *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
  *          "span_outputs" outputs per launch (1..4, default 4) of an evolve whose registers all

@@ -2535,10 +2535,14 @@ int dse_observables(dse_ctx* ctx, int problem, const double* psi, double* obs7) 
 
 // ---- spanning registers (dse_span.hip) ------------------------------------------------------
 
-// option span_tile = -1: the automatic choice takes the smallest of these tiles whose workgroups
-// all fit the chip at once -- 2^10 (a lone N = 14 register over 16 CUs: 78 vs 85 ms at 150 kHz)
-// one per CU, else 2^11 at the kernel's occupancy (one GPU's share of a strong split)
-constexpr int kSpanAutoTiles[2] = {10, 11};
+// option span_tile = -1: the automatic choice takes the first of these (tile bits, resident
+// launches) whose workgroups fit: 2^10 tiles one per CU, all at once (a lone N = 14 register over
+// 16 CUs: 78 vs 85 ms at 150 kHz); 2^11 at the kernel's occupancy, all at once (one GPU's share of
+// an 8-GPU strong split); 2^11 in two resident launches per interval (span_cuts; the registers in
+// degree order, so the stiff ones share the first): one GPU's share of a 4-GPU split, 169 against
+// 225 ms on k_interval, while three launches (a 2-GPU share) lose, 246 against 234 ms
+// (profiles/r06/span_chunks_shard{4,2}.jsonl)
+constexpr int kSpanAutoTiles[3][2] = {{10, 1}, {11, 1}, {11, 2}};
 
 // amplitudes per thread of k_span for an L-bit tile: 2^rb (option span_rb, else 512 threads)
 int span_rb_for(const dse_ctx* ctx, int L) { return ctx->span_rb > 0 ? ctx->span_rb : L - 9; }
@@ -2753,14 +2757,15 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   bool any_dist = false;
   // spanning registers (options span / span_tile): every register that fits runs on k_span over
   // 2^s tiles.  span_tile = -1 (default, auto): when the context's registers are few enough that
-  // all their 2^11-amplitude tiles fit the chip at once (one GPU's share of a strong split, a lone
-  // simulate_rare register), a shorter chain per register; otherwise none spans
+  // all their 2^11-amplitude tiles fit the chip in at most two resident launches (one GPU's share
+  // of a 4- or 8-GPU strong split, a lone simulate_rare register), a shorter chain per register;
+  // otherwise none spans (kSpanAutoTiles)
   {
     int tile = ctx->span_tile;
     if (tile < 0) {
       tile = 0;
-      for (int ti = 0; ti < 2 && tile == 0; ++ti) {
-        const int L = kSpanAutoTiles[ti];
+      for (int ti = 0; ti < 3 && tile == 0; ++ti) {
+        const int L = kSpanAutoTiles[ti][0], chunks = kSpanAutoTiles[ti][1];
         int64_t wg = 0;
         bool all = persistent && ctx->span == 0;
         for (auto& P : ctx->probs) {
@@ -2771,7 +2776,7 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
         }
         int per_cu = 1;
         if (ti > 0 && span_occupancy(L, span_rb_for(ctx, L), true, &per_cu) != hipSuccess) per_cu = 0;
-        if (all && wg > 0 && wg <= (int64_t)per_cu * ctx->n_cu) tile = L;
+        if (all && wg > 0 && wg <= (int64_t)chunks * per_cu * ctx->n_cu) tile = L;
       }
     }
     for (auto& P : ctx->probs) {

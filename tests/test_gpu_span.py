@@ -123,3 +123,20 @@ def test_output_count_options_are_range_checked(engine):
     assert st["span_problems"] == 1 and st["outputs_per_launch"] == 4
     _, st = _evolve(engine, probs, t, span_tile=0)
     assert st["span_problems"] == 0 and st["outputs_per_launch"] == 2
+
+
+def test_automatic_span_policy_strong_split_shares(engine):
+    """span_tile = -1 on one GPU's share of a strong split of the 64-point sweep: the 4-GPU share
+    (16 points = 48 registers, 320 tiles of 2^11) spans in two resident launches per interval (169
+    against 225 ms on k_interval, profiles/r06/span_chunks_shard4.jsonl); the 2-GPU share (96
+    registers, three launches would be needed: 246 against 234 ms) stays on k_interval.  Both agree
+    with span_tile = 0."""
+    t = np.linspace(0.0, 1e-4, 11)
+    dets = np.linspace(0.0, 150e3, 64)
+    for world, rank, spans in ((4, 3, True), (2, 1, False)):
+        probs = [pb.build_problem(_params(v, float(d), t)) for d in dets[rank::world] for v in VARIANTS]
+        auto, st_a = _evolve(engine, probs, t)
+        off, st_o = _evolve(engine, probs, t, span_tile=0)
+        assert st_a["span_problems"] == (len(probs) if spans else 0), (world, st_a["span_problems"])
+        assert st_o["span_problems"] == 0
+        assert float(np.max(np.abs(auto - off))) < 1e-11, world

@@ -5,7 +5,9 @@
                                                 shell_off at 75 / 150 kHz), whole / span_tile 11 / 10
     python3 tools/probe_span.py sweep [reps]    the bench's 192 evolutions with default / span_tile 11 / 10
     python3 tools/probe_span.py shard [reps]    one GPU's share of the 64-point sweep on 8 GPUs
-                                                (8 points = 24 evolutions), default / span_tile 11 / 10
+                                                (8 points = 24 evolutions), default / span_tile 11 / 10;
+                                                SHARD_WORLD=W (default 8) and SHARD_RANK=r (default 0)
+                                                select rank r's share of the W-GPU split
 Grid: config 3's 1 ms / 101 outputs.  Kernel time = HIP events around every interval launch.
 
 Ablation options (ablate, span_ablate, real_ablate) need a diagnostics build of the same ABI:
@@ -106,15 +108,17 @@ def main():
                 run(eng, [p], spans[0], reps, f"center_on_150k_ablate{m}", span_ablate=m)
             eng.set_option("span_ablate", 0)
         else:
-            n_pts = 64 if what == "sweep" else 8
+            world = int(os.environ.get("SHARD_WORLD", "8"))
+            n_pts = 64 if what == "sweep" else 64 // world
             dets = np.linspace(0.0, 150e3, 64)
-            if what == "shard":  # rank 0 of 8 under the strong split: detunings j = 0 mod 8
-                dets = dets[0::8] if os.environ.get("SHARD_RANK") is None else dets[int(os.environ["SHARD_RANK"])::8]
+            if what == "shard":  # rank r of W under the strong split: detunings j = r mod W
+                dets = dets[int(os.environ.get("SHARD_RANK", "0"))::world]
             params = sweep_params(13, dets[:n_pts], T[-1], len(T))
             probs = [pb.build_problem(p) for p in params]
             ref = None
             for s in spans:
-                obs = run(eng, probs, s, reps, what)
+                obs = run(eng, probs, s, reps, what if what == "sweep" else
+                          f"shard{world}_r{os.environ.get('SHARD_RANK', '0')}")
                 if ref is None:
                     ref = obs
                 else:
