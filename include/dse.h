@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DSE_ABI_VERSION 12
+#define DSE_ABI_VERSION 13
 #define DSE_MAX_QUBITS 34
 #define DSE_N_OBS 7
 
@@ -116,6 +116,11 @@ typedef struct dse_stats {
   int32_t eig_fallbacks;      /* dense registers whose two-stage eigensolve gave up a bounded     */
                               /* cross-workgroup poll and were re-solved by rocSOLVER dsyevd     */
                               /* (option "eig_spin_limit"; ABI 12)                                */
+  int32_t dense_nufft_problems; /* dense registers whose output times came from the non-uniform  */
+                              /* FFT instead of the GEMM (option "dense_nufft"; ABI 13)           */
+  int32_t reserved13;
+  double dense_output_ms;     /* host wall time of the dense engine's output stage (refinement,   */
+                              /* transform or GEMM, observables)                                   */
 } dse_stats;
 
 /* ---- library / device ------------------------------------------------------------------- */
@@ -224,6 +229,13 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         polled value; counted in rounds, not time, as spin_limit); a give-up voids that
  *                         solve and the register is re-solved by rocSOLVER dsyevd (stats
  *                         eig_fallbacks); -1: every solve gives up at once (tests)
+ *          "dense_nufft"  dense engine: output times of registers of >= 2^10 amplitudes on a
+ *                         uniform grid (np.linspace: tau_j = j s + delta_j, |delta_j| an ulp) by a
+ *                         type-1 non-uniform FFT of the eigenvalue phases (spreading, rocFFT,
+ *                         deconvolution; ~1e11 flops per 2^14 register) instead of the
+ *                         [cos | -sin] GEMM (4 dim^2 T flops): 1 (default) from 2048 outputs, 2
+ *                         every register from two outputs (tests), 0 never (stats
+ *                         dense_nufft_problems; ABI 13)
  *          "dense_refine" dense engine: 1 (default) eigenvalues refined by double-double
  *                         Rayleigh quotients (exact diagonal) and output phases reduced modulo
  *                         2 pi in double-double; 0 the eigensolver's values and fp64 phases */

@@ -20,7 +20,7 @@ DSE_ERR_CONVERGENCE = -4
 DSE_ERR_STATE = -5
 DSE_ERR_NODEVICE = -6
 DSE_N_OBS = 7
-DSE_ABI_VERSION = 12
+DSE_ABI_VERSION = 13
 
 EXPORTED = (
     "dse_abi_version", "dse_device_count", "dse_spectral_bounds", "dse_bessel_j",
@@ -71,6 +71,9 @@ class DseStats(C.Structure):
         ("matrix_bytes_per_product", C.c_double),
         ("real_problems", C.c_int32),
         ("eig_fallbacks", C.c_int32),
+        ("dense_nufft_problems", C.c_int32),
+        ("reserved13", C.c_int32),
+        ("dense_output_ms", C.c_double),
     ]
 
     def as_dict(self):

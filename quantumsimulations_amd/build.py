@@ -19,7 +19,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdse.so")
 SOURCES = ["dse_kernels.hip", "dse_interval.hip", "dse_wht.hip", "dse_small.hip", "dse_dense.hip", "dse_matrix.hip",
-           "dse_sytrd.hip", "dse_eig2.hip", "dse_span.hip", "dse_real.hip", "dse_runtime.hip", "dse_host.cpp"]
+           "dse_sytrd.hip", "dse_eig2.hip", "dse_span.hip", "dse_real.hip", "dse_nufft.hip", "dse_runtime.hip",
+           "dse_host.cpp"]
 HEADERS = ["dse_internal.h", "dse_device.h", "dse_wht.h", "dse_small.h", "dse_dense.h"]
 ARCH = os.environ.get("DSE_OFFLOAD_ARCH", "gfx950")
 
@@ -64,7 +65,7 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None) ->
             if verbose and (res.stdout or res.stderr):
                 print(res.stdout + res.stderr)
         link = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-L", "/opt/rocm/lib",
-                "-lrccl", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp]
+                "-lrccl", "-lrocsolver", "-lrocblas", "-lrocfft", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp]
         res = subprocess.run(link, capture_output=True, text=True)
         if verbose:
             print(" ".join(link), flush=True)

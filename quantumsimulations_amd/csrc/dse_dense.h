@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
+#include <vector>
 
 namespace dse {
 
@@ -67,6 +69,44 @@ hipError_t launch_state_obs(const DenseProb* d, int dim, const double2* states, 
 // the shift's phase exp(-i shift tau_last) included)
 hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
                               int tb, double tau_last, hipStream_t st);
+// the same two for ONE problem whose tb output columns are interleaved complex (column j = dim
+// double2 at Psi + 2 j dim: the non-uniform FFT's output, dse_nufft.hip)
+hipError_t launch_dense_obs_c(const DenseProb* d, int dim, const double* Psi, int tb, int t0, hipStream_t st);
+hipError_t launch_dense_final_c(const DenseProb* d, int dim, const double* Psi, int tb, double tau_last,
+                                hipStream_t st);
+
+// ---- output times by a type-1 non-uniform FFT (dse_nufft.hip) ---------------------------------
+// On a uniform grid tau_j = j s + delta_j (|delta_j| lambda_max <= 1e-7) psi'(tau_j) of every output
+// from W-point spreading of the eigenvalue phases theta_a = lambda_a s mod 2 pi onto M >= 2T grid
+// points, M-point FFTs per row and deconvolution, instead of the dim^2 T GEMM.
+constexpr int kNufftW = 15;          // kernel width in grid points (error ~3e-14, beta = 2.30 W)
+constexpr int kNufftMinDim = 1024;   // smaller registers keep the GEMM (its cost is small there)
+constexpr int kNufftMinOutputs = 2048;  // option dense_nufft 1: grids of at least this many outputs
+struct NufftGrid {
+  int T = 0, M = 0, half = 0, W = 0;
+  double s = 0.0, h = 0.0, alpha = 0.0, beta = 0.0;
+  std::vector<double> delta;  // tau_j - j s (exact)
+  std::vector<double> scale;  // (2 pi / M) / phi_hat(j - half)
+};
+// false: the grid is not uniform enough (or too short) for the transform
+bool nufft_grid(const double* tau, int n_t, double lam_max, NufftGrid& g);
+struct NufftScratch {  // device buffers of one dense_run (sized for its largest register)
+  double2 *U = nullptr, *U2 = nullptr;  // [M][dim] each
+  double* c = nullptr;                  // [dim]
+  int *off = nullptr, *src = nullptr;   // [M + 1], [nnz_cap]
+  double* wt = nullptr;                 // [4 nnz_cap]
+  size_t nnz_cap = 0;
+  double *scale = nullptr, *delta = nullptr;  // [T] each (uploaded from NufftGrid)
+};
+struct NufftCache;  // rocFFT plans (per context)
+void nufft_release(NufftCache* c);
+size_t nufft_scratch_doubles(const NufftGrid& g, int dim);
+// psi' of every output of one register (V column-major dim x dim, refined eigenvalues, psi0 = e_x0)
+// into Psi in blocks of TB interleaved complex columns, per_block(tb0, tb) called after each block
+// (the observables, the final state); 0 on success
+int nufft_outputs(NufftCache*& cache, hipStream_t st, const NufftGrid& g, const NufftScratch& S, const double* V,
+                  const double* lam_hi, const double* lam_lo, uint64_t x0, int dim, double* Psi, int TB,
+                  const std::function<int(int tb0, int tb)>& per_block);
 
 }  // namespace dse
 

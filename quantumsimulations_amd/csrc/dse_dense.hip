@@ -269,14 +269,15 @@ k_dense_obs(const DenseProb* __restrict__ probs, int dim, const double* __restri
   }
 }
 
+// column tb - 1 of Psi' (layout as k_dense_obs: colstride, imoff, es)
 __global__ void __launch_bounds__(256)
 k_dense_final(const DenseProb* __restrict__ probs, int dim, const double* __restrict__ Psi, size_t pstride,
-              int tb, double tau_last) {
+              size_t colstride, size_t imoff, int es, int tb, double tau_last) {
   const DenseProb& P = probs[blockIdx.y];
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   if (x >= (uint32_t)dim || !P.final_state) return;
-  const double* re = Psi + blockIdx.y * pstride + (size_t)(tb - 1) * dim;
-  const double* im = re + (size_t)tb * dim;
+  const double* re = Psi + blockIdx.y * pstride + (size_t)(tb - 1) * colstride;
+  const double* im = re + imoff;
   // psi_x = exp(-i shift tau) i^{|x0| - |x|} psi'_x   (rot; psi'(0) = e_x0 stands for i^{|x0|} e_x0)
   double s, c;
   if (P.refine)
@@ -288,7 +289,7 @@ k_dense_final(const DenseProb* __restrict__ probs, int dim, const double* __rest
     const double2 q = ipow(__popcll(P.x0) - __popc(x));
     ph = make_double2(ph.x * q.x - ph.y * q.y, ph.x * q.y + ph.y * q.x);
   }
-  const double ar = re[x], ai = im[x];
+  const double ar = re[(size_t)x * es], ai = im[(size_t)x * es];
   P.final_state[x] = make_double2(ph.x * ar - ph.y * ai, ph.x * ai + ph.y * ar);
 }
 
@@ -329,7 +330,20 @@ hipError_t launch_state_obs(const DenseProb* d, int dim, const double2* states, 
 hipError_t launch_dense_final(const DenseProb* d, int count, int dim, const double* Psi, size_t pstride,
                               int tb, double tau_last, hipStream_t st) {
   hipLaunchKernelGGL(k_dense_final, dim3((dim + 255) / 256, count), dim3(256), 0, st, d, dim, Psi,
-                     pstride, tb, tau_last);
+                     pstride, (size_t)dim, (size_t)tb * dim, 1, tb, tau_last);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_obs_c(const DenseProb* d, int dim, const double* Psi, int tb, int t0, hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_obs, dim3(tb, 1), dim3(256), 0, st, d, dim, Psi, (size_t)0, (size_t)2 * dim,
+                     (size_t)1, 2, t0);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_final_c(const DenseProb* d, int dim, const double* Psi, int tb, double tau_last,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(k_dense_final, dim3((dim + 255) / 256, 1), dim3(256), 0, st, d, dim, Psi, (size_t)0,
+                     (size_t)2 * dim, (size_t)1, 2, tb, tau_last);
   return hipGetLastError();
 }
 

@@ -287,6 +287,14 @@ struct dse_ctx {
   // in double-double (option "dense_refine", default 1; 0: the eigensolver's eigenvalues and fp64
   // phases, whose error grows like eps |lambda| t: ~1e-8 at the reference grid's 30 s)
   int dense_refine = 1;
+  // dense engine: output times of registers of >= kNufftMinDim amplitudes by a type-1 non-uniform
+  // FFT on uniform grids (option "dense_nufft": 1 default, from kNufftMinOutputs outputs; 2 every
+  // register from two outputs (tests); 0 the [cos | -sin] GEMM for every output), dse_nufft.hip;
+  // its rocFFT plans
+  int dense_nufft = 1;
+  NufftCache* nufft = nullptr;
+  int nufft_problems = 0;     // last evolve: registers whose outputs came from the transform
+  double dense_out_ms = 0.0;  // last evolve: host wall time of the dense engine's output stage
   std::vector<hipStream_t> eig_st;
   std::vector<rocblas_handle> eig_h;
 };
@@ -507,6 +515,8 @@ void destroy_lanes(dse_ctx* ctx) {
     (void)hipStreamDestroy(ctx->dense_stream);
     ctx->dense_stream = nullptr;
   }
+  nufft_release(ctx->nufft);
+  ctx->nufft = nullptr;
   for (auto& ln : ctx->lanes) {
     if (ln.stream) (void)hipStreamSynchronize(ln.stream);
     if (ln.obs_stream) (void)hipStreamSynchronize(ln.obs_stream);
@@ -1380,6 +1390,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
     ctx->eig_spin = (int)value;
   } else if (k == "dense_refine") {  // dense engine: refined eigenvalues + double-double phases
     ctx->dense_refine = value != 0.0;
+  } else if (k == "dense_nufft") {  // dense engine: output times by the non-uniform FFT (0, 1, 2)
+    if (!(value == 0.0 || value == 1.0 || value == 2.0)) return fail(ctx, DSE_ERR_ARG, "dense_nufft must be 0, 1 or 2");
+    ctx->dense_nufft = (int)value;
   } else if (k == "symv_fused") {  // matrix mode: each product's reduction in the product's launch
     ctx->symv_fused = value != 0.0;
   } else if (k == "dense") {  // dense eigen-propagator engine: 0 off, 1 auto (cost model), 2 always
@@ -1895,8 +1908,10 @@ bool dense_cheaper(const HostProblem& P, const double* t, int n_t, int eig_impl)
 
 struct DevArena {  // device allocations of one dense_run, freed on every exit path
   std::vector<void*> ptrs;
-  ~DevArena() {
+  ~DevArena() { free_all(); }
+  void free_all() {
     for (void* p : ptrs) (void)hipFree(p);
+    ptrs.clear();
   }
   template <typename T>
   T* get(size_t count) {
@@ -1949,6 +1964,43 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
   double* d_tau = arena.get<double>(n_t);
   if (!d_tau) return fail(ctx, DSE_ERR_OOM, "dense engine: allocation failed");
   HIPC(hipMemcpyAsync(d_tau, tau.data(), n_t * sizeof(double), hipMemcpyHostToDevice, st));
+  // the non-uniform FFT's grid and device buffers (sized for the largest eligible register), or none
+  ctx->nufft_problems = 0;
+  NufftGrid ngrid;
+  NufftScratch nscr;
+  DevArena nufft_arena;
+  bool use_nufft = false;
+  if (ctx->dense_nufft && (ctx->dense_nufft == 2 || n_t >= kNufftMinOutputs)) {
+    size_t nmax = 0;
+    double lam_max = 0.0;
+    for (int pi : order) {
+      const HostProblem& P = ctx->probs[pi];
+      if ((size_t(1) << P.n_local) < (size_t)kNufftMinDim && ctx->dense_nufft != 2) continue;
+      nmax = std::max(nmax, size_t(1) << P.n_local);
+      lam_max = std::max({lam_max, std::fabs(P.e_min - P.shift), std::fabs(P.e_max - P.shift)});
+    }
+    if (nmax && nufft_grid(tau.data(), n_t, lam_max, ngrid)) {
+      nscr.U = nufft_arena.get<double2>((size_t)ngrid.M * nmax);
+      nscr.U2 = nufft_arena.get<double2>((size_t)ngrid.M * nmax);
+      nscr.c = nufft_arena.get<double>(nmax);
+      nscr.off = nufft_arena.get<int>((size_t)ngrid.M + 1);
+      nscr.nnz_cap = nmax * (size_t)(kNufftW + 2);
+      nscr.src = nufft_arena.get<int>(nscr.nnz_cap);
+      nscr.wt = nufft_arena.get<double>(4 * nscr.nnz_cap);
+      nscr.scale = nufft_arena.get<double>(n_t);
+      nscr.delta = nufft_arena.get<double>(n_t);
+      use_nufft = nscr.U && nscr.U2 && nscr.c && nscr.off && nscr.src && nscr.wt && nscr.scale && nscr.delta;
+      if (use_nufft) {
+        HIPC(hipMemcpyAsync(nscr.scale, ngrid.scale.data(), n_t * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(nscr.delta, ngrid.delta.data(), n_t * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPC(hipStreamSynchronize(st));
+      } else {  // no room: the GEMM outputs
+        (void)hipGetLastError();
+        nufft_arena.free_all();
+      }
+    }
+  }
+  double out_ms = 0.0;
   struct EigScratch {
     double *A = nullptr, *tau = nullptr, *work = nullptr;
   };
@@ -2177,7 +2229,24 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
           return fail(ctx, DSE_ERR_CONVERGENCE, "dense engine: eigensolver did not converge (info " +
                                                     std::to_string(hinfo[i]) + ")");
       const double one = 1.0, zero = 0.0;
+      const auto o0 = std::chrono::steady_clock::now();
       if (ctx->dense_refine) HIPC(launch_dense_rq(desc, cnt, (int)dim, st));
+      if (use_nufft && (dim >= (size_t)kNufftMinDim || ctx->dense_nufft == 2)) {  // per register, Psi' interleaved
+        for (int i = 0; i < cnt; ++i) {
+          const DenseProb* di = desc + i;
+          auto per_block = [&](int tb0, int tb) -> int {
+            if (launch_dense_obs_c(di, (int)dim, Psi, tb, tb0, st) != hipSuccess) return -1;
+            if (tb0 + tb == n_t && launch_dense_final_c(di, (int)dim, Psi, tb, tau[n_t - 1], st) != hipSuccess)
+              return -1;
+            return 0;
+          };
+          const int rc = nufft_outputs(ctx->nufft, st, ngrid, nscr, V + dim * dim * i, J.lam + dim * (i0 + i),
+                                       J.lam_lo + dim * (i0 + i), ctx->probs[J.list[i0 + i]].psi0, (int)dim, Psi, TB,
+                                       per_block);
+          if (rc) return fail(ctx, DSE_ERR_HIP, "dense engine: non-uniform FFT outputs failed (" + std::to_string(rc) + ")");
+          ctx->nufft_problems++;
+        }
+      } else
       for (int tb0 = 0; tb0 < n_t; tb0 += TB) {
         const int tb = std::min(TB, n_t - tb0);
         HIPC(launch_dense_phase(desc, cnt, (int)dim, d_tau + tb0, tb, Pm, pstride, st));
@@ -2193,6 +2262,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
       std::vector<double> h((size_t)n_t * 8 * cnt);
       HIPC(hipMemcpyAsync(h.data(), J.obs + (size_t)n_t * 8 * i0, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
+      out_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - o0).count();
       for (int i = 0; i < cnt; ++i) {
         const int pi = J.list[i0 + i];
         for (int ti = 0; ti < n_t; ++ti)
@@ -2237,6 +2307,7 @@ int dense_run(dse_ctx* ctx, const double* t, int n_t, double* obs_out, double* m
   }
   if (ms_all) *ms_all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
   if (ms_eig) *ms_eig = eig_ms;
+  ctx->dense_out_ms = out_ms;
   return DSE_OK;
 }
 
@@ -3667,6 +3738,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
     stats->eig_fallbacks = ctx->eig_fallbacks.load();
     stats->dense_ms = dense_ms;
     stats->dense_eig_ms = dense_eig_ms;
+    stats->dense_nufft_problems = any_dense ? ctx->nufft_problems : 0;
+    stats->dense_output_ms = any_dense ? ctx->dense_out_ms : 0.0;
     stats->step_kernel_ms = launches_timed > 0 ? step_ms : -1.0;
     stats->step_launches = launches + small_launches;
     stats->timed_launches = launches_timed;
