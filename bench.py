@@ -120,7 +120,7 @@ def parse():
 # rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench command (tools/gpu.sh traffic +
 # tools/pmc_summary.py), newest round first
 PMC_TRAFFIC = [os.path.join(ROOT, "profiles", r, f) for r, f in
-               (("r05", "bench_pmc_traffic.json"), ("r04", "bench_pmc_traffic.json"), ("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
+               (("r06", "bench_pmc_traffic.json"), ("r05", "bench_pmc_traffic.json"), ("r04", "bench_pmc_traffic.json"), ("r03", "bench_pmc_traffic.json"), ("r02", "bench_pmc_traffic.json"),
                 ("r01", "v9_pmc_traffic.json"))]
 
 
