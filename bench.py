@@ -310,6 +310,7 @@ def full_sweep(eng, probs, n_points: int, intervals: int, repeats: int, sync, di
             "s_per_point": dt / (len(probs) / 3), "dense_problems": dst["dense_problems"],
             "eig_fallbacks": dst.get("eig_fallbacks"),
             "dense_ms": dst["dense_ms"], "eig_ms": dst["dense_eig_ms"],
+            "output_ms": dst.get("dense_output_ms"), "nufft_problems": dst.get("dense_nufft_problems"),
             "tolerance_at_t_final": tolerance_at_t_final(probs, True, t_ref[-1], len(t_ref) - 1),
         })
         if dst["dense_problems"] != len(probs):
@@ -475,7 +476,8 @@ def compact_line(line: dict, detail_path) -> dict:
         tol = fs.get("tolerance_at_t_final", {})
         c["full_sweep"]["tolerance_at_t_final"] = _pick(tol, ("value", "basis", "at_30s"))
         d = fs.get("dense", {})
-        c["full_sweep"]["dense"] = _pick(d, ("s_per_point", "eig_ms", "dense_ms", "eig_fallbacks", "error"))
+        c["full_sweep"]["dense"] = _pick(d, ("s_per_point", "eig_ms", "dense_ms", "output_ms", "nufft_problems",
+                                             "eig_fallbacks", "error"))
         ch = fs.get("chebyshev", {})
         c["full_sweep"]["chebyshev"] = {**_pick(ch, ("value", "full_sweep_s", "timing")),
                                         "tolerance_at_t_final": ch.get("tolerance_at_t_final", {}).get("value")}

@@ -21,7 +21,7 @@ TAG=${1:?tag}; shift
 OUT=gpurun_out/r06/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-LEGS="--no-cpu-baseline --no-large --no-full --no-config2 --no-refdefault"
+LEGS="--no-cpu-baseline --no-large --no-full --no-config2 --no-refdefault --no-shard8"
 step() { echo "[$(date +%T)] $*"; }
 fail() { echo "FAILED: $* (rc $rc)"; exit 1; }
 pmc() {  # name counters...
