@@ -217,8 +217,18 @@ const char* dse_last_error(const dse_ctx* ctx);
  *                         (one simulate_rare call, one GPU's share of a strong split); -1
  *                         (default): when every Chebyshev register of the evolve is 12..15 qubits,
  *                         L = 10 if all their tiles fit one per CU, else L = 11 if they fit the
- *                         chip at once or in two resident launches per interval, else none;
- *                         0 never
+ *                         chip at once; else the partial form (option span_partial); else L = 11
+ *                         in two resident launches per interval; else none; 0 never
+ *          "span_partial" 1 (default): the auto policy's partial form -- when not every register
+ *                         fits spanned in one launch, the registers with the longest predicted
+ *                         chains (spectral half-width x measured term time) span over
+ *                         2^span_partial_tile-amplitude tiles on a stream of their own beside
+ *                         k_interval, as long as every workgroup of both launches fits the chip
+ *                         and the longest chain shrinks by 10% (one GPU's share of a 2- or 4-GPU
+ *                         strong split); 0 off
+ *          "span_chunks"  resident launches per interval the auto policy allows for every
+ *                         register spanned (0, 1, 2; default 2)
+ *          "span_partial_tile"  log2 tile of the partial form (10 or 11, default 11)
  *          "span"         the same with a fixed number s = 1..4 of top bits per register
  *          "span_rb"      k_span's rows per thread 2^span_rb (0: 512 threads per workgroup)
  *          "span_outputs" outputs per launch (1..4, default 4) of an evolve whose registers all

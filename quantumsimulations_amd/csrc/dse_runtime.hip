@@ -169,6 +169,9 @@ struct dse_ctx {
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
   int mixed_launch = 1;             // persistent: 1- and 2-tile problems of one tile size in one launch
+  int span_partial = 1;             // option span_partial: the auto span policy's partial form
+  int span_chunks = 2;              // option span_chunks: resident launches the auto policy allows (0-2)
+  int span_partial_tile = 11;       // option span_partial_tile: the partial form's tile (10, 11)
   int obs_overlap = 0;              // persistent: observables off the interval launches' stream
   int n_cu = 256;                   // compute units of the device
   int coresident = 0;               // diagnostics: workgroups per 2-tile interval chunk (0: occupancy)
@@ -1421,6 +1424,14 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
   } else if (k == "span_rb") {  // amplitudes per thread of k_span: 2^span_rb (0: 512 threads)
     if (!(value >= 0 && value <= 3)) return fail(ctx, DSE_ERR_ARG, "span_rb must be in 0..3");
     ctx->span_rb = (int)value;
+  } else if (k == "span_partial") {  // auto span policy: span the stiffest registers beside k_interval
+    ctx->span_partial = value != 0.0;
+  } else if (k == "span_chunks") {  // auto span policy: resident launches per interval for all-span
+    if (!(value == 0.0 || value == 1.0 || value == 2.0)) return fail(ctx, DSE_ERR_ARG, "span_chunks must be 0, 1 or 2");
+    ctx->span_chunks = (int)value;
+  } else if (k == "span_partial_tile") {  // auto span policy, partial form: log2 tile (10, 11)
+    if (!(value == 10.0 || value == 11.0)) return fail(ctx, DSE_ERR_ARG, "span_partial_tile must be 10 or 11");
+    ctx->span_partial_tile = (int)value;
   } else if (k == "mixed_launch") {
     ctx->mixed_launch = value != 0.0;
   } else if (k == "obs_overlap") {
@@ -2833,9 +2844,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
   // otherwise none spans (kSpanAutoTiles)
   {
     int tile = ctx->span_tile;
-    if (tile < 0) {
-      tile = 0;
-      for (int ti = 0; ti < 3 && tile == 0; ++ti) {
+    // the all-span candidates kSpanAutoTiles[ti0, ti1): the smallest tile whose workgroups fit
+    auto all_span_tile = [&](int ti0, int ti1) {
+      int tl = 0;
+      for (int ti = ti0; ti < ti1 && tl == 0; ++ti) {
         const int L = kSpanAutoTiles[ti][0], chunks = kSpanAutoTiles[ti][1];
         int64_t wg = 0;
         bool all = persistent && ctx->span == 0;
@@ -2847,13 +2859,74 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
         }
         int per_cu = 1;
         if (ti > 0 && span_occupancy(L, span_rb_for(ctx, L), true, &per_cu) != hipSuccess) per_cu = 0;
-        if (all && wg > 0 && wg <= (int64_t)chunks * per_cu * ctx->n_cu) tile = L;
+        if (all && wg > 0 && chunks <= ctx->span_chunks && wg <= (int64_t)chunks * per_cu * ctx->n_cu) tl = L;
+      }
+      return tl;
+    };
+    auto assign = [&]() {
+      for (auto& P : ctx->probs) {
+        const int s = tile > 0 ? P.n_local - tile : ctx->span;
+        P.span_s = (persistent && span_eligible(ctx, P, s)) ? s : 0;
+      }
+    };
+    // order: every register spanned in one resident launch; else the partial span below; else
+    // every register spanned in two resident launches (the partial form measured faster on the
+    // 4-GPU share, 151 against 167 ms, profiles/r06/span_partial_shards.jsonl)
+    if (tile < 0) tile = all_span_tile(0, 2);
+    assign();
+    // Partial span (option span_partial, round 6): when the registers do not all fit spanned (one
+    // GPU's share of a 2-GPU split: 96 registers), the ones with the longest predicted chains span
+    // over 2^11-amplitude tiles on a lane of their own while the rest stay on k_interval, as long
+    // as every workgroup of both launches fits the chip at once (each takes a CU: residency of
+    // every hand-off partner is guaranteed, whatever order the two streams' workgroups land in).
+    // Predicted chain of a register: its spectral half-width (degree per interval ~ alpha dt) times
+    // the measured term time of its kernel under load (kTermUs); applied when the longest chain
+    // shrinks by at least 10%.
+    bool partial = false;
+    if (ctx->span_tile < 0 && tile == 0 && ctx->span == 0 && persistent && ctx->span_partial &&
+        std::min<int>(ctx->n_streams, (int)ctx->probs.size()) >= 2) {
+      const int Lp = ctx->span_partial_tile;
+      // term time under load: k_interval 1-tile, 2-tile; k_span over 2^Lp-amplitude tiles
+      const double kTermUs[3] = {19.5, 24.0, Lp == 11 ? 14.0 : 11.0};
+      struct C {
+        double chain;
+        int pi, kind;  // kind 0 / 1: k_interval of 1 / 2 tiles, 2: spanned
+      };
+      std::vector<C> cs;
+      int64_t wg = 0;
+      bool ok = true;
+      for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
+        const HostProblem& P = ctx->probs[pi];
+        if (P.side()) continue;
+        if (P.shard_bits != 0 || !(P.n_tiles == 1 || P.n_tiles == 2) || !interval_supported(P.L)) ok = false;
+        wg += P.n_tiles;
+        const double alpha = 0.5 * (P.e_max - P.e_min);
+        cs.push_back({alpha * kTermUs[P.n_tiles - 1], (int)pi, (int)P.n_tiles - 1});
+      }
+      auto worst = [&]() { return std::max_element(cs.begin(), cs.end(), [](const C& a, const C& b) { return a.chain < b.chain; }); };
+      if (ok && !cs.empty() && wg <= ctx->n_cu) {
+        const double before = worst()->chain;
+        std::vector<int> spanned;
+        for (;;) {
+          auto w = worst();
+          if (w->kind == 2) break;
+          const HostProblem& P = ctx->probs[w->pi];
+          const int sp = P.n_local - Lp;
+          if (!span_eligible(ctx, P, sp)) break;
+          const int64_t extra = (int64_t(1) << sp) - P.n_tiles;
+          if (wg + extra > ctx->n_cu) break;
+          wg += extra;
+          w->chain = w->chain / kTermUs[w->kind] * kTermUs[2];
+          w->kind = 2;
+          spanned.push_back(w->pi);
+        }
+        if (!spanned.empty() && worst()->chain <= 0.9 * before) {
+          for (int pi : spanned) ctx->probs[pi].span_s = ctx->probs[pi].n_local - Lp;
+          partial = true;
+        }
       }
     }
-    for (auto& P : ctx->probs) {
-      const int s = tile > 0 ? P.n_local - tile : ctx->span;
-      P.span_s = (persistent && span_eligible(ctx, P, s)) ? s : 0;
-    }
+    if (ctx->span_tile < 0 && tile == 0 && !partial && (tile = all_span_tile(2, 3)) > 0) assign();
   }
   for (auto& P : ctx->probs) {
     if (P.side()) continue;
@@ -3219,6 +3292,8 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
                                                                 : (mixed ? 0 : P.n_tiles));
     int lane = (int)(i % n_lanes);
     if (persistent) lane = (P.n_tiles == 2 || n_lanes == 1 || mixed || P.span_s || P.rl) ? 0 : 1;
+    // partial span: the spanned registers on a lane of their own, concurrent with k_interval's
+    if (persistent && P.span_s && !all_span && n_lanes >= 2) lane = n_lanes >= 3 ? 2 : 1;
     // shards of one register read each other's vectors: same lane, hence the same launches
     if (P.shard_bits > 0 && !P.dist) lane = P.group_first % n_lanes;
     lane_probs[lane][key].push_back(order[i]);

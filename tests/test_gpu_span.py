@@ -114,7 +114,8 @@ def test_automatic_span_policy(engine):
 def test_output_count_options_are_range_checked(engine):
     """span_outputs takes 1..4 (k_span staggers the sums); outputs_per_launch stays 1..2 (k_interval
     and k_real hold the sums of one term in registers); a bad value is refused, the old one kept."""
-    for key, bad in (("span_outputs", 5), ("span_outputs", 0), ("outputs_per_launch", 3)):
+    for key, bad in (("span_outputs", 5), ("span_outputs", 0), ("outputs_per_launch", 3),
+                     ("span_chunks", 3), ("span_partial_tile", 12), ("span_partial_tile", 9)):
         with pytest.raises(ValueError):
             engine.set_option(key, bad)
     t = np.linspace(0.0, 1e-4, 11)
@@ -126,17 +127,21 @@ def test_output_count_options_are_range_checked(engine):
 
 
 def test_automatic_span_policy_strong_split_shares(engine):
-    """span_tile = -1 on one GPU's share of a strong split of the 64-point sweep: the 4-GPU share
-    (16 points = 48 registers, 320 tiles of 2^11) spans in two resident launches per interval (169
-    against 225 ms on k_interval, profiles/r06/span_chunks_shard4.jsonl); the 2-GPU share (96
-    registers, three launches would be needed: 246 against 234 ms) stays on k_interval.  Both agree
-    with span_tile = 0."""
+    """span_tile = -1 on one GPU's share of a strong split of the 64-point sweep.  The 8-GPU share
+    (24 registers) spans whole in one resident launch; the 4-GPU share (48 registers) and the 2-GPU
+    share (96) take the partial form: the stiffest registers span over 2^11-amplitude tiles on a
+    lane of their own beside k_interval (4-GPU: 151 against 167 ms for all spanned in two launches;
+    2-GPU: 212 against 233 ms on k_interval alone, profiles/r06/span_partial_shards.jsonl).  All
+    agree with span_tile = 0."""
     t = np.linspace(0.0, 1e-4, 11)
     dets = np.linspace(0.0, 150e3, 64)
-    for world, rank, spans in ((4, 3, True), (2, 1, False)):
+    for world, rank in ((8, 7), (4, 3), (2, 1)):
         probs = [pb.build_problem(_params(v, float(d), t)) for d in dets[rank::world] for v in VARIANTS]
         auto, st_a = _evolve(engine, probs, t)
         off, st_o = _evolve(engine, probs, t, span_tile=0)
-        assert st_a["span_problems"] == (len(probs) if spans else 0), (world, st_a["span_problems"])
+        if world == 8:
+            assert st_a["span_problems"] == len(probs), (world, st_a["span_problems"])
+        else:
+            assert 0 < st_a["span_problems"] < len(probs), (world, st_a["span_problems"])
         assert st_o["span_problems"] == 0
         assert float(np.max(np.abs(auto - off))) < 1e-11, world

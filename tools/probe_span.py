@@ -33,7 +33,8 @@ T = np.linspace(0.0, 1e-3, 101)
 def setting(span):
     """'+'-joined tokens: '0' whole registers (span_tile 0), 'a' the automatic policy (default),
     'tL' option span_tile L, 'sS' option span S, 'rX' option real X (e.g. '0+r0': k_interval),
-    'bB' option span_rb B (2^B amplitudes per thread), 'mM' option span_outputs M"""
+    'bB' option span_rb B (2^B amplitudes per thread), 'mM' option span_outputs M, 'pP' option
+    span_partial P, 'cC' option span_chunks C, 'qL' option span_partial_tile L"""
     opts = {}
     for tok in str(span).split("+"):
         if tok == "0":
@@ -41,7 +42,8 @@ def setting(span):
         elif tok == "a":
             opts["span_tile"] = -1
         else:
-            opts[{"t": "span_tile", "s": "span", "r": "real", "b": "span_rb", "m": "span_outputs"}[tok[0]]] = int(tok[1:])
+            opts[{"t": "span_tile", "s": "span", "r": "real", "b": "span_rb", "m": "span_outputs",
+                  "p": "span_partial", "c": "span_chunks", "q": "span_partial_tile"}[tok[0]]] = int(tok[1:])
     return opts
 
 
@@ -65,6 +67,9 @@ def run(eng, probs, span, reps, label, **opts):
     eng.set_option("real", 0)
     eng.set_option("span_rb", 0)
     eng.set_option("span_outputs", 4)
+    eng.set_option("span_partial", 1)
+    eng.set_option("span_chunks", 2)
+    eng.set_option("span_partial_tile", 11)
     eng.clear()
     terms = st["h_applications"]
     rec = {"case": label, "span": span, "n_probs": len(probs), "wall_ms": min(walls),
