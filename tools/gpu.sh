@@ -11,6 +11,7 @@
 #   trace                      rocprofv3 --kernel-trace --stats of the bench's sweep leg
 #   traffic                    FETCH_SIZE and WRITE_SIZE passes of the same (one counter per run)
 #   traffic_large              the same over tools/bench_large.py (N = 30, Walsh-Hadamard engine)
+#   large_trace[:args]         rocprofv3 kernel trace of tools/bench_large.py <args> (per-pass times)
 #   sq:<set>                   three SQ counter passes over tools/probe_one.py <set>
 #   sqeig:<dim>                the same over tools/bin/probe_eig2 <dim> (PMC_FILTER: a kernel regex)
 #   sytrd:<dim,...>            tools/bin/probe_sytrd <dim> check
@@ -59,6 +60,10 @@ for T in "$@"; do
       [ $rc -eq 0 ] || fail fetch_large
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/large/write -o write --output-format csv -- python3 tools/bench_large.py --steps 3 > $OUT/large_write.json 2> $OUT/large_write.err; rc=$?
       [ $rc -eq 0 ] || fail write_large ;;
+    large_trace)  # large_trace:<bench_large args>: kernel trace of the N = 30 register (per-pass times)
+      nl=$((nl + 1))
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/large_trace_$nl -o large --output-format csv -- python3 tools/bench_large.py "${A[@]}" > $OUT/large_trace_$nl.json 2> $OUT/large_trace_$nl.err; rc=$?
+      echo "${A[*]}" > $OUT/large_trace_$nl.args; tail -c 400 $OUT/large_trace_$nl.json; [ $rc -eq 0 ] || fail large_trace ;;
     sq|sqeig)  # sqeig:<dim>: the same passes over tools/bin/probe_eig2 <dim>
       PMC_CMD=(python3 tools/probe_one.py "${A[@]}"); q=$(echo "${A[*]}" | tr ' =' '__')_
       [ $task = sqeig ] && PMC_CMD=(tools/bin/probe_eig2 "${A[@]}") && q=eig2_${q}
