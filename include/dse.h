@@ -180,6 +180,10 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "wht_persist"  Walsh-Hadamard engine: bit 1 runs MID as a persistent launch (one
  *                         workgroup per CU looping over tiles, next tile's loads under the other
  *                         vector's transposes); 0 (default)
+ *          "wht_half"     Walsh-Hadamard engine, 13-bit tiles: passes with one vector in registers
+ *                         and the LDS transposes in halves (real, then imaginary parts), two
+ *                         workgroups per CU: bit 0 FIRST, bit 1 FWD / INV, bit 2 MID (default 7;
+ *                         0 the one-workgroup-per-CU passes); results bitwise identical
  *          "dense"        dense eigen-propagator: 0 off, 1 by cost model (default), 2 always
  *          "eig_streams"  dense engine: eigendecompositions of registers of >= 2^10 amplitudes
  *                         run this many at a time, one stream and rocBLAS handle each, 1..8

@@ -165,6 +165,7 @@ struct dse_ctx {
   int wht_group_bits = 0;           // high bits per pass of that engine (0: tile bits - 2)
   int wht_tile_bits = 0;            // its tile: 12, 13 (0 = 13)
   int wht_persist = 0;              // bit 1: MID as a persistent launch (k_wht_mid_p), option wht_persist
+  int wht_half = 7;                 // option wht_half: half-LDS passes (k_wht_h), bit 0 FIRST, 1 FWD/INV, 2 MID
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
   int xcd_pairs = 1;                // diagnostics: 0 keeps the two tiles of a problem adjacent
@@ -1076,7 +1077,7 @@ int wht_run(dse_ctx* ctx, int wl, int G, const std::vector<std::pair<const int2*
   auto part = [&](int pt, int vsel) -> int {
     for (const auto& sg : segs)
       HIPC(launch_wht_part(pt, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, vsel, st,
-                           ctx->n_cu * (wl == 13 ? 1 : 2), ctx->wht_persist));
+                           ctx->n_cu * (wl == 13 ? 1 : 2), ctx->wht_persist | ctx->wht_half << 8));
     return DSE_OK;
   };
   if (regs.empty() || !ctx->swap_overlap) {
@@ -1344,6 +1345,9 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
       free_device(ctx);
       ctx->wht = value != 0.0;
     }
+  } else if (k == "wht_half") {  // Walsh-Hadamard passes through half the LDS, two workgroups per CU
+    if (!(value >= 0.0 && value <= 7.0 && value == (int)value)) return fail(ctx, DSE_ERR_ARG, "wht_half must be 0..7");
+    ctx->wht_half = (int)value;
   } else if (k == "wht_persist") {  // Walsh-Hadamard passes as persistent launches: bit 1 MID
     ctx->wht_persist = (int)value;
   } else if (k == "wht_tile_bits") {

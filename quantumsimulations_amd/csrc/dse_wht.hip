@@ -128,37 +128,70 @@ __device__ __forceinline__ void transpose(double2* lds, double2* v, int tid) {
   for (int r = 0; r < WR; ++r) v[r] = rp[slot<WL, PAD>(tau_of<WL>(TO, r, 0))];
 }
 
+// The same layout change through half the LDS: the real parts, then the imaginary parts, each a
+// ds_write_b64 / ds_read_b64 transpose of 8-byte slots (the slot map is conflict-free for these
+// too: 4 LDS-array cycles per write, 2 per read, every transpose at WL = 13).  A 13-bit tile then
+// takes 68 KiB, so two workgroups share a CU and one's HBM traffic runs under the other's
+// transposes (option wht_half).
+template <int WL, int FROM, int TO>
+__device__ __forceinline__ void transpose_h(double* lds, double2* v, int tid) {
+  constexpr bool PAD = FROM == 2 || TO == 2;
+  asm volatile("" : "+v"(tid));  // the LDS bases are computed here, not held from kernel entry
+  double* wp = lds + slot<WL, PAD>(tau_of<WL>(FROM, 0, tid));
+  const double* rp = lds + slot<WL, PAD>(tau_of<WL>(TO, 0, tid));
+  __syncthreads();  // the previous transpose's reads are done
+#pragma unroll
+  for (int r = 0; r < WR; ++r) wp[slot<WL, PAD>(tau_of<WL>(FROM, r, 0))] = v[r].x;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < WR; ++r) v[r].x = rp[slot<WL, PAD>(tau_of<WL>(TO, r, 0))];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < WR; ++r) wp[slot<WL, PAD>(tau_of<WL>(FROM, r, 0))] = v[r].y;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < WR; ++r) v[r].y = rp[slot<WL, PAD>(tau_of<WL>(TO, r, 0))];
+}
+
+template <int WL, bool H, int FROM, int TO>
+__device__ __forceinline__ void xpose(void* lds, double2* v, int tid) {
+  if constexpr (H)
+    transpose_h<WL, FROM, TO>((double*)lds, v, tid);
+  else
+    transpose<WL, FROM, TO>((double2*)lds, v, tid);
+}
+
 template <int WL>
 __device__ __forceinline__ void layout_wht(double2* v, int lay, int c, int tid) {
   reg_wht(v, active_mask<WL>(lay, c));
   if (WL == 13 && lay == 2 && c == 0) lane0_wht(v, tid);
 }
 // forward transform of a group (c carried bits) from layout A; returns the layout it ends in
-template <int WL>
-__device__ __forceinline__ int tile_fwd(double2* lds, double2* v, int c, int tid) {
+template <int WL, bool H = false>
+__device__ __forceinline__ int tile_fwd(void* lds, double2* v, int c, int tid) {
   layout_wht<WL>(v, 0, c, tid);
   if (!has_b<WL>(c)) return 0;
   if (has_c<WL>(c)) {
-    transpose<WL, 0, 2>(lds, v, tid);
+    xpose<WL, H, 0, 2>(lds, v, tid);
     layout_wht<WL>(v, 2, c, tid);
-    transpose<WL, 2, 1>(lds, v, tid);
+    xpose<WL, H, 2, 1>(lds, v, tid);
   } else {
-    transpose<WL, 0, 1>(lds, v, tid);
+    xpose<WL, H, 0, 1>(lds, v, tid);
   }
   layout_wht<WL>(v, 1, c, tid);
   return 1;
 }
 // the same butterflies from layout `last` (tile_fwd's result) back to layout A
-template <int WL>
-__device__ __forceinline__ void tile_back(double2* lds, double2* v, int c, int last, int tid) {
+template <int WL, bool H = false>
+__device__ __forceinline__ void tile_back(void* lds, double2* v, int c, int last, int tid) {
   if (last == 1) {
     layout_wht<WL>(v, 1, c, tid);
     if (has_c<WL>(c)) {
-      transpose<WL, 1, 2>(lds, v, tid);
+      xpose<WL, H, 1, 2>(lds, v, tid);
       layout_wht<WL>(v, 2, c, tid);
-      transpose<WL, 2, 0>(lds, v, tid);
+      xpose<WL, H, 2, 0>(lds, v, tid);
     } else {
-      transpose<WL, 1, 0>(lds, v, tid);
+      xpose<WL, H, 1, 0>(lds, v, tid);
     }
   }
   layout_wht<WL>(v, 0, c, tid);
@@ -168,6 +201,11 @@ template <int WL>
 struct WhtShared {
   double2 w[WG<WL>::SLOTS];
   double f[2][WL + 1];  // MID: D_X, D_Y fields per tile bit + constant; FINAL: D_Z (z convention)
+};
+template <int WL>
+struct WhtSharedH {  // half-LDS passes (transpose_h)
+  double w[WG<WL>::SLOTS];
+  double f[2][WL + 1];
 };
 
 // size of one pair form in WhtProb::qtab
@@ -530,6 +568,161 @@ k_wht_mid_p(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprob
   }
 }
 
+// Half-LDS passes (option wht_half): FIRST, FWD / INV and MID with one vector in registers at a
+// time and the transposes through transpose_h, so two workgroups (at most 128 VGPRs each) share a
+// CU and one's loads and stores run under the other's transposes -- the one-workgroup-per-CU form
+// leaves each tile's compute unoverlapped apart from the second vector's loads.  FIRST reads the
+// tile of w twice (A from it, then B from S^+ w: the second read mostly from the caches) instead
+// of holding both vectors.  Same arithmetic, same order: bitwise identical to k_wht.
+
+// tile_fwd / tile_back with the layout path fixed at compile time (PATH 2: A -> C -> B, 1: A -> B,
+// 0: no transpose; tile_path(c)), so the register arrays take no copies where paths would merge
+__host__ __device__ constexpr int tile_path13(int c) { return c < 5 ? 2 : (c < 9 ? 1 : 0); }
+template <int WL, int PATH>
+__device__ __forceinline__ void tile_fwd_p(double* lds, double2* v, int c, int tid) {
+  layout_wht<WL>(v, 0, c, tid);
+  if constexpr (PATH == 2) {
+    transpose_h<WL, 0, 2>(lds, v, tid);
+    layout_wht<WL>(v, 2, c, tid);
+    transpose_h<WL, 2, 1>(lds, v, tid);
+  } else if constexpr (PATH == 1) {
+    transpose_h<WL, 0, 1>(lds, v, tid);
+  }
+  if constexpr (PATH > 0) layout_wht<WL>(v, 1, c, tid);
+}
+template <int WL, int PATH>
+__device__ __forceinline__ void tile_back_p(double* lds, double2* v, int c, int tid) {
+  if constexpr (PATH > 0) layout_wht<WL>(v, 1, c, tid);
+  if constexpr (PATH == 2) {
+    transpose_h<WL, 1, 2>(lds, v, tid);
+    layout_wht<WL>(v, 2, c, tid);
+    transpose_h<WL, 2, 0>(lds, v, tid);
+  } else if constexpr (PATH == 1) {
+    transpose_h<WL, 1, 0>(lds, v, tid);
+  }
+  layout_wht<WL>(v, 0, c, tid);
+}
+
+// an opaque copy: values derived from it are recomputed, not kept live across a transform
+__device__ __forceinline__ uint64_t launder(uint64_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// offset of register r from a LayIdx's per-thread part (wave-uniform bits)
+template <int WL>
+__device__ __forceinline__ uint64_t roff(const LayIdx<WL>& L, int r) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if ((r >> i) & 1) x |= L.rb[i];
+  return x;
+}
+
+// FWD / INV / MID of one vector through half the LDS (k_wht_h), layout path fixed
+template <int WL, int PASS, int PATH>
+__device__ __forceinline__ void wht_h_vec(WhtSharedH<WL>& S, const WhtProb& W, const WhtGroup& G, uint64_t o,
+                                          int vec, int tid) {
+  constexpr int last = PATH > 0 ? 1 : 0;
+  double2 v[WR];
+  const uint64_t xo = outer_bits(G, o);
+  gd2* X = gptr(PASS == WHT_MID ? (vec == 0 ? W.vec_at : W.vec_bt) : (vec == 0 ? W.vec_a : W.vec_b));
+  {
+    const LayIdx<WL> ia(G, 0, tid, launder(xo));
+#pragma unroll
+    for (int r = 0; r < WR; ++r) v[r] = gld(X, ia.xt | roff<WL>(ia, r));
+  }
+  tile_fwd_p<WL, PATH>(S.w, v, G.c, tid);
+  if constexpr (PASS == WHT_MID) {
+    if constexpr (PATH == 0) __syncthreads();  // no transpose ran: S.f
+    double qt, qh[4];
+    pair_parts<WL>(W.qtab, tid, qt, qh);
+    const double* zr = W.qtab + 5 * WG<WL>::NT;
+    const double sg = vec == 0 ? 1.0 : -1.0;
+    double lt, lh[4];
+    lin_parts<WL>(S.f[vec], last, tid, lt, lh);
+    lt += sg * qt;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lh[i] += sg * qh[i];
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      const double d = quad_at(lt, lh, zr[r], sg, r);
+      v[r].x *= d;
+      v[r].y *= d;
+    }
+    tile_back_p<WL, PATH>(S.w, v, G.c, tid);
+    const LayIdx<WL> is(G, 0, tid, launder(xo));
+#pragma unroll
+    for (int r = 0; r < WR; ++r) gst(X, is.xt | roff<WL>(is, r), v[r]);
+  } else {
+    const LayIdx<WL> is(G, last, tid, launder(xo));
+#pragma unroll
+    for (int r = 0; r < WR; ++r) gst(X, is.xt | roff<WL>(is, r), v[r]);
+  }
+}
+
+template <int WL, int PASS, int MODE, int VSEL>
+__global__ void __launch_bounds__(WG<WL>::NT, 4 * WG<WL>::NT / 512)  // two workgroups per CU: <= 128 VGPRs at WL = 13
+k_wht_h(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, const int2* __restrict__ items,
+        int g, int k, int q, int set) {
+  static_assert(WL == 13, "half-LDS passes: 13-bit tiles (12-bit tiles already fit two workgroups per CU)");
+  __shared__ WhtSharedH<WL> S;
+  const int2 it = items[blockIdx.x];
+  const WhtProb& W = probs[it.x];
+  const DevProb& P = dprobs[it.x];
+  const int tid = threadIdx.x;
+  if (MODE == MODE_GEN && k > P.degree) return;  // uniform
+  const WhtGroup& G = W.grp[g];
+  const uint64_t o = (uint64_t)(uint32_t)it.y;
+  if constexpr (PASS == WHT_FIRST) {
+    double2 v[WR];
+    const uint64_t xa = (o << WL) | (uint64_t)tau_of<WL>(0, 0, tid);  // LayIdx0: x = xt | tau(lay, r, 0)
+    const gd2* win = gptr((const double2*)P.buf[win_role(MODE, k, q)]);
+#pragma unroll
+    for (int r = 0; r < WR; ++r) v[r] = gld(win, xa | (uint64_t)tau_of<WL>(0, r, 0));
+    tile_fwd_p<WL, 2>(S.w, v, 0, tid);
+    {
+      const uint64_t xs = launder((o << WL) | (uint64_t)tau_of<WL>(1, 0, tid));
+      gd2* A = gptr(W.vec_a);
+#pragma unroll
+      for (int r = 0; r < WR; ++r) gst(A, xs | (uint64_t)tau_of<WL>(1, r, 0), v[r]);
+    }
+    {
+      const uint64_t xb = launder(xa);
+#pragma unroll
+      for (int r = 0; r < WR; ++r) {
+        const uint64_t x = xb | (uint64_t)tau_of<WL>(0, r, 0);
+        v[r] = mul_ipow(gld(win, x), -(__popcll(x) + W.phase0));
+      }
+    }
+    tile_fwd_p<WL, 2>(S.w, v, 0, tid);
+    {
+      const uint64_t xs = launder((o << WL) | (uint64_t)tau_of<WL>(1, 0, tid));
+      gd2* B = gptr(W.vec_b);
+#pragma unroll
+      for (int r = 0; r < WR; ++r) gst(B, xs | (uint64_t)tau_of<WL>(1, r, 0), v[r]);
+    }
+  } else {
+    if constexpr (PASS == WHT_MID) {
+      if (tid < 32) {  // read after the first forward transform's barriers
+        const double c = gptr((const double*)W.xytab)[o * 32 + tid];
+        if (tid <= WL) S.f[0][tid] = c;
+        else if (tid >= 16 && tid <= 16 + WL) S.f[1][tid - 16] = c;
+      }
+    }
+    const int path = tile_path13(G.c);  // uniform
+#pragma unroll
+    for (int vec = 0; vec < 2; ++vec) {
+      if (!((VSEL >> vec) & 1)) continue;
+      if (path == 2)
+        wht_h_vec<WL, PASS, 2>(S, W, G, o, vec, tid);
+      else if (path == 1)
+        wht_h_vec<WL, PASS, 1>(S, W, G, o, vec, tid);
+      else
+        wht_h_vec<WL, PASS, 0>(S, W, G, o, vec, tid);
+    }
+  }
+}
+
 // One thread per tile o: D_Z pieces of group-0 tile o (tile_diag_coeffs without beta) and the
 // D_X / D_Y pieces of MID-group tile o:  F_q = lin(pos_q) + sum_i c(pos_q, opos_i) z_i,
 // C = sum_i lin(opos_i) z_i + sum_{i<j} c(opos_i, opos_j) z_i z_j  (D_Y: lin_y, -c).
@@ -644,10 +837,35 @@ hipError_t launch_pass_v(int mode, const WhtProb* wp, const DevProb* dp, const i
   return hipGetLastError();
 }
 
-// FIRST and FINAL always take both vectors; FWD / MID / INV one (vsel 1, 2) or both (3)
+template <int WL, int PASS, int VSEL>
+hipError_t launch_pass_h(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
+                         int g, int k, int q, int set, hipStream_t st) {
+  const dim3 grid(n_items), block(WG<WL>::NT);
+  if (mode == MODE_APPLY)
+    hipLaunchKernelGGL((k_wht_h<WL, PASS, MODE_APPLY, VSEL>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+  else if (mode == MODE_FIRST)
+    hipLaunchKernelGGL((k_wht_h<WL, PASS, MODE_FIRST, VSEL>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+  else
+    hipLaunchKernelGGL((k_wht_h<WL, PASS, MODE_GEN, VSEL>), grid, block, 0, st, wp, dp, items, g, k, q, set);
+  return hipGetLastError();
+}
+
+// FIRST and FINAL always take both vectors; FWD / MID / INV one (vsel 1, 2) or both (3).  half:
+// the half-LDS form (k_wht_h; not FINAL, which holds both transformed vectors)
 template <int WL, int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
-                       int g, int k, int q, int set, int vsel, hipStream_t st) {
+                       int g, int k, int q, int set, int vsel, hipStream_t st, bool half = false) {
+  if constexpr (PASS != WHT_FINAL && WL == 13) {
+    if (half) {
+      if constexpr (PASS == WHT_FIRST) {
+        return launch_pass_h<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
+      } else {
+        if (vsel == 3) return launch_pass_h<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
+        if (vsel == 1) return launch_pass_h<WL, PASS, 1>(mode, wp, dp, items, n_items, g, k, q, set, st);
+        return launch_pass_h<WL, PASS, 2>(mode, wp, dp, items, n_items, g, k, q, set, st);
+      }
+    }
+  }
   if constexpr (PASS == WHT_FIRST || PASS == WHT_FINAL) {
     return launch_pass_v<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
   } else {
@@ -674,6 +892,11 @@ template <int WL>
 hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const DevProb* dp, const int2* items,
                     int n_items, int k, int q, int set, int vsel, hipStream_t st, int pgrid, int pmask) {
   hipError_t e = hipSuccess;
+  // pmask: option wht_persist (bit 1 persistent MID) | option wht_half << 8 (bit 0 FIRST, bit 1
+  // FWD / INV, bit 2 MID)
+  const int half = pmask >> 8;
+  if (part == WHT_PART_MID && (half & 4))
+    return launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, vsel, st, true);
   if (part == WHT_PART_MID && pgrid > 0 && (pmask & 2)) {  // persistent MID
     const int g = n_groups - 1;
     if (vsel == 3) return launch_mid_p<WL, 3>(mode, wp, dp, items, n_items, g, k, pgrid, st);
@@ -681,14 +904,14 @@ hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const D
     return launch_mid_p<WL, 2>(mode, wp, dp, items, n_items, g, k, pgrid, st);
   }
   if (part == WHT_PART_PRE) {
-    if (vsel & 1) e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
+    if (vsel & 1) e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st, half & 1);
     for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
-      e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st);
+      e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st, half & 2);
   } else if (part == WHT_PART_MID) {
     e = launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, vsel, st);
   } else {
     for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
-      e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st);
+      e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st, half & 2);
     if (e == hipSuccess && (vsel & 2))
       e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
   }

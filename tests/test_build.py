@@ -53,7 +53,7 @@ def test_interval_kernel_does_not_spill(tmp_path):
 
 def test_wht_passes_do_not_spill(tmp_path):
     """The Walsh-Hadamard passes (2 tile sizes x 5 passes x 3 modes, FWD / MID / INV also per
-    vector of a partitioned register) stay spill-free and keep their tile arrays out of scratch
+    vector of a partitioned register; the half-LDS forms of option wht_half within 128 VGPRs) stay spill-free and keep their tile arrays out of scratch
     (a run-time vector selector once put them there: N = 30 went from 68 to 353 ms per H); the
     one-thread-per-tile table kernels run once per problem and may use scratch."""
     res = subprocess.run(
@@ -64,10 +64,13 @@ def test_wht_passes_do_not_spill(tmp_path):
     assert res.returncode == 0, res.stderr[-2000:]
     kernels = [k for k in _resources(res.stderr) if "k_wht" in k[0]]
     persistent = [k for k in kernels if "k_wht_mid_p" in k[0]]
-    passes = [k for k in kernels if "k_wht_tables" not in k[0] and "k_wht_qtab" not in k[0] and k not in persistent]
+    half = [k for k in kernels if "k_wht_h" in k[0]]
+    passes = [k for k in kernels if "k_wht_tables" not in k[0] and "k_wht_qtab" not in k[0] and k not in persistent
+              and k not in half]
     assert len(passes) == 2 * (2 * 3 + 3 * 3 * 3), [k[0] for k in passes]
     assert len(persistent) == 2 * 3 * 3, [k[0] for k in persistent]  # tile x mode x vectors
-    passes += persistent
+    assert len(half) == 3 + 3 * 3 * 3, [k[0] for k in half]  # 13-bit tiles: FIRST x mode, FWD/MID/INV x mode x vectors
+    passes += persistent + half
     assert all(sp == 0 for _, sp, _ in kernels), kernels
     assert all(sc == 0 for _, _, sc in passes), passes
 

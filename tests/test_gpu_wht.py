@@ -234,6 +234,7 @@ def test_wht_persistent_mid_is_bitwise_identical(engine, n, tile_bits, shard_bit
     out = {}
     try:
         engine.set_option("wht_tile_bits", tile_bits)
+        engine.set_option("wht_half", 0)  # the half-LDS MID would take the pass
         for pm in (0, 2):
             engine.clear()
             engine.set_option("wht_persist", pm)
@@ -245,6 +246,37 @@ def test_wht_persistent_mid_is_bitwise_identical(engine, n, tile_bits, shard_bit
     finally:
         engine.clear()
         engine.set_option("wht_persist", 0)
+        engine.set_option("wht_half", 7)
         engine.set_option("wht_tile_bits", 0)
     assert np.array_equal(out[0][0], out[2][0])
     assert np.array_equal(out[0][1], out[2][1])
+
+
+@pytest.mark.parametrize("n,shard_bits", [(17, 0), (20, 0), (22, 0), (26, 0), (20, 2), (26, 1)])
+def test_wht_half_lds_passes_are_bitwise_identical(engine, n, shard_bits):
+    """Option wht_half (k_wht_h: FIRST, FWD / INV and MID with one vector in registers and the
+    transposes through half the LDS, real then imaginary parts, two workgroups per CU) moves the
+    same values through LDS and does the same butterflies in the same order as k_wht, so results
+    agree bit for bit -- every layout path (MID group c = 9, 6, 4 at n = 17, 20, 22; FWD / INV at
+    n = 26), whole and partitioned registers (one vector per launch under swap overlap).  N = 30
+    (tools/bench_large.py, one box): 74.1 -> 63.4 ms per H application, FIRST 12.2 -> 10.0, FWD / INV
+    14.0 -> 11.2, MID 16.6 -> 13.3 ms (profiles/r06/wht_half_n30_kernel_stats_*.csv)."""
+    prob = _random_problem(n, 2300 + n, rare_bit=n - 1)
+    t = np.linspace(0.0, 2e-4, 4)
+    out = {}
+    try:
+        engine.set_option("wht_tile_bits", 13)
+        for hm in (0, 7):
+            engine.clear()
+            engine.set_option("wht_half", hm)
+            ps = engine.add_sharded(prob, shard_bits) if shard_bits else engine.add(prob)
+            obs, st = engine.evolve(t)
+            assert st["mode"] == 2
+            k = 1 << shard_bits
+            out[hm] = (obs[ps:ps + k].copy(), engine.state(ps))
+    finally:
+        engine.clear()
+        engine.set_option("wht_half", 7)
+        engine.set_option("wht_tile_bits", 0)
+    assert np.array_equal(out[0][0], out[7][0])
+    assert np.array_equal(out[0][1], out[7][1])
