@@ -165,6 +165,7 @@ struct dse_ctx {
   int wht_group_bits = 0;           // high bits per pass of that engine (0: tile bits - 2)
   int wht_tile_bits = 0;            // its tile: 12, 13 (0 = 13)
   int wht_persist = 0;              // bit 1: MID as a persistent launch (k_wht_mid_p), option wht_persist
+  int wht_mid_inpage = 0;           // option wht_mid_inpage: in-page high bits of the MID group
   int wht_half = 7;                 // option wht_half: half-LDS passes (k_wht_h), bit 0 FIRST, 1 FWD/INV, 2 MID
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
   bool wht_ready = false;
@@ -842,7 +843,14 @@ std::vector<std::vector<int>> split_bits(const std::vector<int>& bits, int max_b
 // the last one is MID's.  Partitioned (S shard bits): the pre-swap groups must transform the top
 // S local bits T (they leave with the index swap); MID transforms the shard bits that arrive in
 // T's positions together with up to max_bits - S other local high bits.
-int wht_layout(int n_local, int S, int wl, int max_bits, WhtProb& w) {
+//
+// mid_inpage m > 0 (option wht_mid_inpage, unpartitioned registers): the MID group takes the top m
+// high bits below the 2-MiB page (local bits < kWhtPageBit) in place of its lowest above-page
+// bits, the other groups the rest.  A pass's tile touches 2^(its group's above-page bits) pages;
+// with the contiguous split MID's group lies wholly above the page (N = 30: 256 pages per tile,
+// a TLB miss on 61% of its requests) while FWD's keeps every in-page bit (32 pages).
+constexpr int kWhtPageBit = 17;  // 2^17 amplitudes of 16 B = 2 MiB
+int wht_layout(int n_local, int S, int wl, int max_bits, WhtProb& w, int mid_inpage = 0) {
   const int h = n_local - wl;
   if (h < 1 || h > kWhtMaxOuter || h < S || max_bits <= S) return 0;
   std::vector<int> high;
@@ -850,6 +858,21 @@ int wht_layout(int n_local, int S, int wl, int max_bits, WhtProb& w) {
   std::vector<std::vector<int>> groups;
   if (S == 0) {
     groups = split_bits(high, max_bits);
+    if (mid_inpage > 0 && groups.size() >= 2) {
+      std::vector<int> inpage, above;
+      for (int b : high) (b < kWhtPageBit ? inpage : above).push_back(b);
+      const int smid = (int)groups.back().size();
+      const int m = std::min({mid_inpage, (int)inpage.size(), smid});
+      if (m > 0 && (int)above.size() >= smid - m) {
+        std::vector<int> mid(inpage.end() - m, inpage.end());
+        mid.insert(mid.end(), above.end() - (smid - m), above.end());
+        std::vector<int> rest;
+        for (int b : high)
+          if (std::find(mid.begin(), mid.end(), b) == mid.end()) rest.push_back(b);
+        groups = split_bits(rest, max_bits);
+        groups.push_back(mid);
+      }
+    }
   } else {
     const std::vector<int> rest(high.begin(), high.end() - S), T(high.end() - S, high.end());
     const int m = std::min(max_bits - S, (int)rest.size());
@@ -880,7 +903,7 @@ int ensure_wht(dse_ctx* ctx) {
     const int n = p.n, nl = p.n_local, S = p.shard_bits;
     WhtProb& w = hw[pi];
     const int gb = ctx->wht_group_bits ? std::min(ctx->wht_group_bits, p.L - 2) : p.L - 2;
-    const int G = wht_layout(nl, S, p.L, gb, w);
+    const int G = wht_layout(nl, S, p.L, gb, w, ctx->wht_mid_inpage);
     if (G < 2) continue;
     const double sc = std::ldexp(1.0, -n);
     std::vector<double> cq(size_t(n) * n, 0.0);
@@ -1345,6 +1368,13 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
       free_device(ctx);
       ctx->wht = value != 0.0;
     }
+  } else if (k == "wht_mid_inpage") {  // Walsh-Hadamard plan: MID group's high bits below the page
+    if (!(value >= 0.0 && value <= 8.0 && value == (int)value)) return fail(ctx, DSE_ERR_ARG, "wht_mid_inpage must be 0..8");
+    if ((int)value != ctx->wht_mid_inpage) {
+      (void)sync_all(ctx);
+      free_device(ctx);
+      ctx->wht_mid_inpage = (int)value;
+    }
   } else if (k == "wht_half") {  // Walsh-Hadamard passes through half the LDS, two workgroups per CU
     if (!(value >= 0.0 && value <= 7.0 && value == (int)value)) return fail(ctx, DSE_ERR_ARG, "wht_half must be 0..7");
     ctx->wht_half = (int)value;
@@ -1619,8 +1649,9 @@ int dse_wht_plan(int n_local, int shard_bits, int tile_bits, int max_bits, int32
     return DSE_ERR_ARG;
   WhtProb w;
   std::memset(&w, 0, sizeof(w));
-  const int gb = max_bits ? std::min(max_bits, tile_bits - 2) : tile_bits - 2;
-  const int G = wht_layout(n_local, shard_bits, tile_bits, gb, w);
+  const int mb = max_bits & 0xff;  // bits 8-15: the MID group's in-page bits (option wht_mid_inpage)
+  const int gb = mb ? std::min(mb, tile_bits - 2) : tile_bits - 2;
+  const int G = wht_layout(n_local, shard_bits, tile_bits, gb, w, (max_bits >> 8) & 0xff);
   for (int g = 0; g < G; ++g) {
     groups_out[g * 14] = w.grp[g].c;
     for (int q = 0; q < tile_bits; ++q) groups_out[g * 14 + 1 + q] = w.grp[g].pos[q];

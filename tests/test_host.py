@@ -266,15 +266,25 @@ def _wht_plan(n_local, shard_bits, wl, max_bits=0):
 
 
 @pytest.mark.parametrize("wl", [12, 13])
-@pytest.mark.parametrize("shard_bits", [0, 1, 2, 3])
-def test_wht_pass_plans_transform_every_bit_once(wl, shard_bits):
+@pytest.mark.parametrize("shard_bits,mid_inpage", [(0, 0), (1, 0), (2, 0), (3, 0), (0, 2), (0, 4)])
+def test_wht_pass_plans_transform_every_bit_once(wl, shard_bits, mid_inpage):
     """Walsh-Hadamard pass plans (csrc/dse_runtime.hip wht_layout): group 0 is the low tile; every
     local bit is transformed once (the MID group's top-S positions carry the arriving shard bits,
     so the top S local bits must leave through an earlier group); carried bits are the lowest ones
-    and groups respect the size limit."""
+    and groups respect the size limit.  mid_inpage (option wht_mid_inpage, passed in max_bits'
+    second byte): the MID group holds that many high bits below the 2-MiB page (local bit 17)
+    when there are that many, the group sizes unchanged."""
     for n_local in range(wl + 1, 35 - shard_bits):
         for max_bits in (0, 2, 4, 7, 11):
-            G, groups = _wht_plan(n_local, shard_bits, wl, max_bits)
+            G, groups = _wht_plan(n_local, shard_bits, wl, max_bits | mid_inpage << 8)
+            if mid_inpage and G >= 3:
+                G0, groups0 = _wht_plan(n_local, shard_bits, wl, max_bits)
+                assert sorted(wl - c for c, _ in groups) == sorted(wl - c for c, _ in groups0)
+                c, pos = groups[-1]
+                inpage = [b for b in range(wl, min(17, n_local))]
+                m = min(mid_inpage, len(inpage), wl - c)
+                if n_local - 17 >= wl - c - m:
+                    assert sum(1 for b in pos[c:] if b < 17) == m, (n_local, max_bits, groups)
             mb = min(max_bits or wl - 2, wl - 2)
             h = n_local - wl
             if shard_bits == 0:
