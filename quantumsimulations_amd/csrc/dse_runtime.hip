@@ -2933,7 +2933,10 @@ static int evolve_impl(dse_ctx* ctx, const double* t, int n_t, double tol, doubl
       for (size_t pi = 0; pi < ctx->probs.size(); ++pi) {
         const HostProblem& P = ctx->probs[pi];
         if (P.side()) continue;
-        if (P.shard_bits != 0 || !(P.n_tiles == 1 || P.n_tiles == 2) || !interval_supported(P.L)) ok = false;
+        if (P.shard_bits != 0 || !(P.n_tiles == 1 || P.n_tiles == 2) || !interval_supported(P.L)) {
+          ok = false;  // (and kTermUs has entries for 1- and 2-tile registers only)
+          break;
+        }
         wg += P.n_tiles;
         const double alpha = 0.5 * (P.e_max - P.e_min);
         cs.push_back({alpha * kTermUs[P.n_tiles - 1], (int)pi, (int)P.n_tiles - 1});

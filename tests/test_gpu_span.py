@@ -145,3 +145,16 @@ def test_automatic_span_policy_strong_split_shares(engine):
             assert 0 < st_a["span_problems"] < len(probs), (world, st_a["span_problems"])
         assert st_o["span_problems"] == 0
         assert float(np.max(np.abs(auto - off))) < 1e-11, world
+
+
+def test_automatic_span_policy_skips_contexts_with_larger_registers(engine):
+    """The partial form's chain model covers 1- and 2-tile registers only: a context holding
+    several larger registers (here two N = 16 registers, four tiles each, on the Walsh-Hadamard
+    engine) leaves the policy before it prices them (round 6: an out-of-range table read there
+    crashed the N = 30 loopback-shard test) and spans nothing."""
+    t = np.linspace(0.0, 2e-5, 3)
+    probs = [pb.build_problem(sweep_point_params(15, 75e3, v, float(t[-1]), len(t))) for v in ("center_on", "shell_off")]
+    assert all(p.n_qubits == 16 for p in probs)
+    obs, st = _evolve(engine, probs, t)
+    assert st["span_problems"] == 0
+    np.testing.assert_allclose(obs[:, 6], 1.0, atol=1e-12)
