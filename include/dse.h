@@ -180,6 +180,12 @@ const char* dse_last_error(const dse_ctx* ctx);
  *          "wht_persist"  Walsh-Hadamard engine: bit 1 runs MID as a persistent launch (one
  *                         workgroup per CU looping over tiles, next tile's loads under the other
  *                         vector's transposes); 0 (default)
+ *          "wht_fuse"     Walsh-Hadamard engine, unpartitioned registers: 1 (default) the FINAL pass
+ *                         of term k also runs term k + 1's FIRST on the new vector while it is in
+ *                         registers (one read of it and one launch less per term; the group-0
+ *                         butterflies in another order: results agree to rounding); 0 separate
+ *          "wht_mid_inpage"  Walsh-Hadamard plan: the MID group's high bits below the 2-MiB page
+ *                         (0 default; measured slower, kept for experiments)
  *          "wht_half"     Walsh-Hadamard engine, 13-bit tiles: passes with one vector in registers
  *                         and the LDS transposes in halves (real, then imaginary parts), two
  *                         workgroups per CU: bit 0 FIRST, bit 1 FWD / INV, bit 2 MID (default 7;

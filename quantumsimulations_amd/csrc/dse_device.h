@@ -102,12 +102,14 @@ __device__ __forceinline__ void stage16(void* dst, const void* src, int n16, int
 __device__ __forceinline__ double2 gld(const double2* p, size_t i) { return p[i]; }
 __device__ __forceinline__ void gst(double2* p, size_t i, double2 a) { p[i] = a; }
 
+// (returns the value stored to wdst: the new vector, for a caller that keeps it)
 template <int MODE, typename Ptr>
-__device__ __forceinline__ void step_epilogue(size_t x, double2 out, double2 own, double scale,
-                                              Ptr __restrict__ wdst, Ptr __restrict__ acc_b,
-                                              const CoefK& C, int no_reads) {
+__device__ __forceinline__ double2 step_epilogue(size_t x, double2 out, double2 own, double scale,
+                                                 Ptr __restrict__ wdst, Ptr __restrict__ acc_b,
+                                                 const CoefK& C, int no_reads) {
   if (MODE == MODE_APPLY) {
     gst(wdst, x, out);
+    return out;
   } else if (MODE == MODE_FIRST) {
     double2 w;
     w.x = scale * out.x;
@@ -117,6 +119,7 @@ __device__ __forceinline__ void step_epilogue(size_t x, double2 out, double2 own
     a = cmad(a, C.c[1].x, C.c[1].y, own);
     a = cmad(a, C.c[2].x, C.c[2].y, w);
     gst(acc_b, x, a);
+    return w;
   } else {
     const double2 prev = no_reads ? make_double2(0.0, 0.0) : gld(wdst, x);
     double2 w;
@@ -130,6 +133,7 @@ __device__ __forceinline__ void step_epilogue(size_t x, double2 out, double2 own
       a = cmad(a, C.c[2].x, C.c[2].y, w);
       gst(acc_b, x, a);
     }
+    return w;
   }
 }
 

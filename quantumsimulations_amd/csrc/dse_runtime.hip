@@ -165,6 +165,8 @@ struct dse_ctx {
   int wht_group_bits = 0;           // high bits per pass of that engine (0: tile bits - 2)
   int wht_tile_bits = 0;            // its tile: 12, 13 (0 = 13)
   int wht_persist = 0;              // bit 1: MID as a persistent launch (k_wht_mid_p), option wht_persist
+  int wht_contiguous = 0;           // option wht_contiguous: hipDeviceMallocContiguous X/Y vectors
+  int wht_fuse = 1;                 // option wht_fuse: FINAL of term k runs term k + 1's FIRST
   int wht_mid_inpage = 0;           // option wht_mid_inpage: in-page high bits of the MID group
   int wht_half = 7;                 // option wht_half: half-LDS passes (k_wht_h), bit 0 FIRST, 1 FWD/INV, 2 MID
   WhtProb* d_wht = nullptr;         // per problem (zero entries: not on that engine)
@@ -919,7 +921,15 @@ int ensure_wht(dse_ctx* ctx) {
     const int nvec = S > 0 ? 4 : 2;
     bool ok = hipMalloc(&p.d_cquad, cq.size() * sizeof(double)) == hipSuccess &&
               hipMalloc(&p.d_wtab, ((size_t)p.n_tiles * 48 + 2 * (5 * 512 + 16)) * sizeof(double)) == hipSuccess;
-    for (int v = 0; v < nvec && ok; ++v) ok = hipMalloc(&p.wvec[v], vbytes) == hipSuccess;
+    // option wht_contiguous: the X/Y-branch vectors physically contiguous (large translation
+    // fragments for the strided passes), else (or when that fails) a plain allocation
+    for (int v = 0; v < nvec && ok; ++v) {
+      if (ctx->wht_contiguous &&
+          hipExtMallocWithFlags((void**)&p.wvec[v], vbytes, hipDeviceMallocContiguous) == hipSuccess)
+        continue;
+      (void)hipGetLastError();
+      ok = hipMalloc(&p.wvec[v], vbytes) == hipSuccess;
+    }
     if (!ok) {  // HBM too small for the engine's two extra vectors: this problem keeps the step kernels
       (void)hipGetLastError();
       free_wht(p);
@@ -1100,7 +1110,8 @@ int wht_run(dse_ctx* ctx, int wl, int G, const std::vector<std::pair<const int2*
   auto part = [&](int pt, int vsel) -> int {
     for (const auto& sg : segs)
       HIPC(launch_wht_part(pt, wl, mode, G, ctx->d_wht, ctx->d_probs, sg.first, sg.second, k, q, set, vsel, st,
-                           ctx->n_cu * (wl == 13 ? 1 : 2), ctx->wht_persist | ctx->wht_half << 8));
+                           ctx->n_cu * (wl == 13 ? 1 : 2),
+                           ctx->wht_persist | ctx->wht_half << 8 | (ctx->wht_fuse && regs.empty()) << 16));
     return DSE_OK;
   };
   if (regs.empty() || !ctx->swap_overlap) {
@@ -1368,6 +1379,16 @@ int dse_set_option(dse_ctx* ctx, const char* key, double value) {
       free_device(ctx);
       ctx->wht = value != 0.0;
     }
+  } else if (k == "wht_contiguous") {  // Walsh-Hadamard engine's vectors physically contiguous
+    if (!(value == 0.0 || value == 1.0)) return fail(ctx, DSE_ERR_ARG, "wht_contiguous must be 0 or 1");
+    if ((int)value != ctx->wht_contiguous) {
+      (void)sync_all(ctx);
+      free_device(ctx);
+      ctx->wht_contiguous = (int)value;
+    }
+  } else if (k == "wht_fuse") {  // Walsh-Hadamard engine: FINAL of term k + FIRST of term k + 1
+    if (!(value == 0.0 || value == 1.0)) return fail(ctx, DSE_ERR_ARG, "wht_fuse must be 0 or 1");
+    ctx->wht_fuse = (int)value;
   } else if (k == "wht_mid_inpage") {  // Walsh-Hadamard plan: MID group's high bits below the page
     if (!(value >= 0.0 && value <= 8.0 && value == (int)value)) return fail(ctx, DSE_ERR_ARG, "wht_mid_inpage must be 0..8");
     if ((int)value != ctx->wht_mid_inpage) {

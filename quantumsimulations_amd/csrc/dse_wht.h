@@ -6,7 +6,9 @@
 
 namespace dse {
 
-enum { WHT_FIRST = 0, WHT_FWD = 1, WHT_MID = 2, WHT_INV = 3, WHT_FINAL = 4 };
+// WHT_FINAL_NEXT: FINAL of term k, then the next term's FIRST from the new w_k still in registers
+// (option wht_fuse)
+enum { WHT_FIRST = 0, WHT_FWD = 1, WHT_MID = 2, WHT_INV = 3, WHT_FINAL = 4, WHT_FINAL_NEXT = 5 };
 
 constexpr int kWhtMinTile = 12;                       // tile bits of the passes: 12 or 13
 constexpr int kWhtMaxTile = 13;

@@ -240,6 +240,12 @@ __device__ __forceinline__ double quad_at(double zt, const double* hr, double zr
   return d;
 }
 
+// an opaque copy: values derived from it are recomputed, not kept live across a transform
+__device__ __forceinline__ uint64_t launder(uint64_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // v * i^k
 __device__ __forceinline__ double2 mul_ipow(double2 v, int k) {
   switch (k & 3) {
@@ -417,8 +423,11 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
     return;
   }
 
-  // ---- FINAL (group 0 tile = ordinary tile h): out = D_Z w + W0 A + S W0 B, then the recurrence
-  if (PASS == WHT_FINAL) {
+  // ---- FINAL (group 0 tile = ordinary tile h): out = D_Z w + W0 A + S W0 B, then the recurrence;
+  // FINAL_NEXT then runs the next term's FIRST on the new w_k while it is in registers: A = W0 w_k,
+  // B = W0 S^+ w_k, transformed from layout B back to A (the butterflies of a transform commute,
+  // so the order only changes the rounding), saving FIRST's read of w_k and its launch
+  if (PASS == WHT_FINAL || PASS == WHT_FINAL_NEXT) {
     constexpr int last = 1;  // group 0 ends every forward transform in layout B
     const LayIdx0<WL> ia0(0, tid, o);
     // D_Z in the z convention: fields F_i / 2 and constant C(h) - beta per tile (ztab), the in-tile
@@ -470,7 +479,35 @@ k_wht(const WhtProb* __restrict__ probs, const DevProb* __restrict__ dprobs, con
       const double d = quad_at(zt, hr, zrz[r], 1.0, r);
       out[r].x = fma(d, own.x, out[r].x);
       out[r].y = fma(d, own.y, out[r].y);
-      step_epilogue<MODE>(is[r], out[r], own, scale, wdst, acc_b, C, 0);
+      const double2 w = step_epilogue<MODE>(is[r], out[r], own, scale, wdst, acc_b, C, 0);
+      if constexpr (PASS == WHT_FINAL_NEXT) out[r] = w;
+    }
+    if constexpr (PASS == WHT_FINAL_NEXT && MODE != MODE_APPLY) {
+      if (k < P.degree) {  // uniform: the next term exists for this register
+        asm volatile("" : : : "memory");  // the epilogue's stores first: its registers free for v
+        int t2 = tid;  // indices recomputed from an opaque copy, not held from the kernel's start
+        asm volatile("" : "+v"(t2));
+        {
+          const uint64_t xb = (o << WL) | (uint64_t)tau_of<WL>(last, 0, t2);
+#pragma unroll
+          for (int r = 0; r < WR; ++r)  // S^+
+            v[r] = mul_ipow(out[r], -(__popcll(xb | (uint64_t)tau_of<WL>(last, r, 0)) + W.phase0));
+        }
+        tile_back<WL>(S.w, out, 0, last, tid);  // B -> C -> A
+        {
+          const uint64_t xa = (o << WL) | (uint64_t)tau_of<WL>(0, 0, t2);
+          gd2* A = gptr(W.vec_a);
+#pragma unroll
+          for (int r = 0; r < WR; ++r) gst(A, xa | (uint64_t)tau_of<WL>(0, r, 0), out[r]);
+        }
+        tile_back<WL>(S.w, v, 0, last, tid);
+        {
+          const uint64_t xa = launder((o << WL) | (uint64_t)tau_of<WL>(0, 0, t2));
+          gd2* B = gptr(W.vec_b);
+#pragma unroll
+          for (int r = 0; r < WR; ++r) gst(B, xa | (uint64_t)tau_of<WL>(0, r, 0), v[r]);
+        }
+      }
     }
   }
 }
@@ -603,11 +640,6 @@ __device__ __forceinline__ void tile_back_p(double* lds, double2* v, int c, int 
   layout_wht<WL>(v, 0, c, tid);
 }
 
-// an opaque copy: values derived from it are recomputed, not kept live across a transform
-__device__ __forceinline__ uint64_t launder(uint64_t x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
 // offset of register r from a LayIdx's per-thread part (wave-uniform bits)
 template <int WL>
 __device__ __forceinline__ uint64_t roff(const LayIdx<WL>& L, int r) {
@@ -631,11 +663,11 @@ __device__ __forceinline__ void wht_h_vec(WhtSharedH<WL>& S, const WhtProb& W, c
 #pragma unroll
     for (int r = 0; r < WR; ++r) v[r] = gld(X, ia.xt | roff<WL>(ia, r));
   }
+  double qt = 0.0, qh[4] = {0.0, 0.0, 0.0, 0.0};
+  if constexpr (PASS == WHT_MID) pair_parts<WL>(W.qtab, tid, qt, qh);  // in flight under the transform
   tile_fwd_p<WL, PATH>(S.w, v, G.c, tid);
   if constexpr (PASS == WHT_MID) {
     if constexpr (PATH == 0) __syncthreads();  // no transpose ran: S.f
-    double qt, qh[4];
-    pair_parts<WL>(W.qtab, tid, qt, qh);
     const double* zr = W.qtab + 5 * WG<WL>::NT;
     const double sg = vec == 0 ? 1.0 : -1.0;
     double lt, lh[4];
@@ -855,7 +887,7 @@ hipError_t launch_pass_h(int mode, const WhtProb* wp, const DevProb* dp, const i
 template <int WL, int PASS>
 hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int2* items, int n_items,
                        int g, int k, int q, int set, int vsel, hipStream_t st, bool half = false) {
-  if constexpr (PASS != WHT_FINAL && WL == 13) {
+  if constexpr (PASS != WHT_FINAL && PASS != WHT_FINAL_NEXT && WL == 13) {
     if (half) {
       if constexpr (PASS == WHT_FIRST) {
         return launch_pass_h<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
@@ -866,7 +898,7 @@ hipError_t launch_pass(int mode, const WhtProb* wp, const DevProb* dp, const int
       }
     }
   }
-  if constexpr (PASS == WHT_FIRST || PASS == WHT_FINAL) {
+  if constexpr (PASS == WHT_FIRST || PASS == WHT_FINAL || PASS == WHT_FINAL_NEXT) {
     return launch_pass_v<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
   } else {
     if (vsel == 3) return launch_pass_v<WL, PASS, 3>(mode, wp, dp, items, n_items, g, k, q, set, st);
@@ -894,7 +926,8 @@ hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const D
   hipError_t e = hipSuccess;
   // pmask: option wht_persist (bit 1 persistent MID) | option wht_half << 8 (bit 0 FIRST, bit 1
   // FWD / INV, bit 2 MID)
-  const int half = pmask >> 8;
+  const int half = (pmask >> 8) & 0xff;
+  const bool fuse = (pmask >> 16) & 1;  // option wht_fuse: FINAL_NEXT, and no FIRST past term 1
   if (part == WHT_PART_MID && (half & 4))
     return launch_pass<WL, WHT_MID>(mode, wp, dp, items, n_items, n_groups - 1, k, q, set, vsel, st, true);
   if (part == WHT_PART_MID && pgrid > 0 && (pmask & 2)) {  // persistent MID
@@ -904,7 +937,8 @@ hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const D
     return launch_mid_p<WL, 2>(mode, wp, dp, items, n_items, g, k, pgrid, st);
   }
   if (part == WHT_PART_PRE) {
-    if (vsel & 1) e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st, half & 1);
+    if ((vsel & 1) && !(fuse && mode == MODE_GEN))
+      e = launch_pass<WL, WHT_FIRST>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st, half & 1);
     for (int g = 1; e == hipSuccess && g + 1 < n_groups; ++g)
       e = launch_pass<WL, WHT_FWD>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st, half & 2);
   } else if (part == WHT_PART_MID) {
@@ -912,8 +946,12 @@ hipError_t wht_part(int part, int mode, int n_groups, const WhtProb* wp, const D
   } else {
     for (int g = n_groups - 2; e == hipSuccess && g >= 1; --g)
       e = launch_pass<WL, WHT_INV>(mode, wp, dp, items, n_items, g, k, q, set, vsel, st, half & 2);
-    if (e == hipSuccess && (vsel & 2))
-      e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
+    if (e == hipSuccess && (vsel & 2)) {
+      if (fuse && mode != MODE_APPLY)
+        e = launch_pass<WL, WHT_FINAL_NEXT>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
+      else
+        e = launch_pass<WL, WHT_FINAL>(mode, wp, dp, items, n_items, 0, k, q, set, 3, st);
+    }
   }
   return e;
 }

@@ -280,3 +280,33 @@ def test_wht_half_lds_passes_are_bitwise_identical(engine, n, shard_bits):
         engine.set_option("wht_tile_bits", 0)
     assert np.array_equal(out[0][0], out[7][0])
     assert np.array_equal(out[0][1], out[7][1])
+
+
+@pytest.mark.parametrize("n", [20, 22, 26])
+def test_wht_fused_final_first_matches_unfused(engine, n):
+    """Option wht_fuse: the FINAL pass of term k also runs term k + 1's FIRST on the new w_k while it
+    is in registers (no re-read of w_k, one launch less per term).  The group-0 transform then runs
+    B -> C -> A instead of A -> C -> B -- the same butterflies in another order -- so results agree
+    with the unfused passes to rounding, and both with the step kernels."""
+    prob = _random_problem(n, 2400 + n, rare_bit=n - 1)
+    t = np.linspace(0.0, 2e-4, 4)
+    out = {}
+    try:
+        for fu in (0, 1):
+            engine.clear()
+            engine.set_option("wht_fuse", fu)
+            pid = engine.add(prob)
+            obs, st = engine.evolve(t)
+            assert st["mode"] == 2
+            out[fu] = obs[pid].copy()
+        engine.clear()
+        engine.set_option("wht", 0)
+        pid = engine.add(prob)
+        ref, _ = engine.evolve(t)
+        ref = ref[pid]
+    finally:
+        engine.clear()
+        engine.set_option("wht", 1)
+        engine.set_option("wht_fuse", 1)
+    assert float(np.max(np.abs(out[1] - out[0]))) < 1e-12
+    assert float(np.max(np.abs(out[1] - ref))) < 1e-11

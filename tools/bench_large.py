@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--wht-group-bits", type=int, default=0)
     ap.add_argument("--wht-tile-bits", type=int, default=0)
     ap.add_argument("--wht-persist", type=int, default=0, help="option wht_persist (bit 1: persistent MID)")
+    ap.add_argument("--wht-contiguous", type=int, default=-1, help="option wht_contiguous; -1 the default")
+    ap.add_argument("--wht-fuse", type=int, default=-1, help="option wht_fuse (FINAL + next FIRST); -1 the default")
     ap.add_argument("--wht-mid-inpage", type=int, default=-1,
                     help="option wht_mid_inpage (MID group's high bits below the 2-MiB page); -1 the default")
     ap.add_argument("--wht-half", type=int, default=-1,
@@ -55,6 +57,10 @@ def main():
         eng.set_option("wht_persist", a.wht_persist)
         if a.wht_half >= 0:
             eng.set_option("wht_half", a.wht_half)
+        if a.wht_contiguous >= 0:
+            eng.set_option("wht_contiguous", a.wht_contiguous)
+        if a.wht_fuse >= 0:
+            eng.set_option("wht_fuse", a.wht_fuse)
         if a.wht_mid_inpage >= 0:
             eng.set_option("wht_mid_inpage", a.wht_mid_inpage)
         eng.add(prob)
@@ -79,7 +85,7 @@ def main():
         "step_kernel_gbs_algorithmic": gbs, "hbm_peak_gbs": 8000.0,
         "step_kernel_fp64_tflops": tfl, "fp64_peak_tflops": 78.6,
         "mode": st["mode"], "wht_group_bits": a.wht_group_bits, "wht_tile_bits": a.wht_tile_bits,
-        "wht_persist": a.wht_persist, "wht_half": a.wht_half, "wht_mid_inpage": a.wht_mid_inpage,
+        "wht_persist": a.wht_persist, "wht_half": a.wht_half, "wht_mid_inpage": a.wht_mid_inpage, "wht_fuse": a.wht_fuse, "wht_contiguous": a.wht_contiguous,
         "max_degree": st["max_degree"], "tile_bits": st["tile_bits"],
         "norm_drift": float(np.max(np.abs(norm - 1.0))),
         "obs_t_final": {k: float(obs[0, i, -1]) for i, k in enumerate(pb.OBS_NAMES)},
