@@ -832,6 +832,9 @@ def main():
     eng.set_option("span_tile", args.span_tile)
     if os.environ.get("DSE_CORESIDENT"):  # diagnostics: workgroups per 2-tile interval launch chunk
         eng.set_option("coresident", float(os.environ["DSE_CORESIDENT"]))
+    for kv in filter(None, os.environ.get("DSE_BENCH_SET", "").split(",")):  # A/Bs: key=value,...
+        key, val = kv.split("=")
+        eng.set_option(key, float(val))
     for p in probs:
         eng.add(p)
 
