@@ -49,3 +49,12 @@ def test_lds_bytes_per_amp_term_matches_the_kernel_schedule():
     # 16 amplitudes per thread; per term 9 x (16 + 64 + 8) + 19 + 16 ds_read_b128 and 16 ds_write_b128
     assert bench.LDS_B_PER_AMP_TERM == 16.0 * (9 * 88 + 51) / 16.0
     assert abs(bench.LDS_PEAK_TBS - 157.3) < 0.1
+
+
+def test_clock_under_load_record_is_read():
+    """roofline.on_chip.clock: the GPU clock under the bench's full sweep from the committed
+    GRBM_GUI_ACTIVE record (tools/clock_probe.sh), below the nominal 2.4 GHz and below the clock of
+    one GPU's 2-GPU share (the chip power-caps with every CU busy)."""
+    clk = bench.clock_under_load()
+    assert clk is not None
+    assert 1.0 < clk["full_sweep_ghz"] < clk["share2_ghz"] <= 2.4

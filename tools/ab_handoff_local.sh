@@ -1,3 +1,4 @@
+# (round 6 A/B; the option handoff_local was removed after it: no change in time or traffic)
 # A/B of option handoff_local on the bench's sweep leg (step time, k_interval launch time), then
 # FETCH_SIZE passes per setting (tools/pmc_summary.py reads gpurun_out/r06/x2/<setting>/).
 set -o pipefail
