@@ -40,6 +40,8 @@ Extra fields of the JSON line:
                  wall time is the N-GPU step time (ms/ODE-step beside it)
 The stdout line is a compact summary (< 4 KB: the driver keeps the tail of stdout); the full record,
 per-shard arrays and tolerance detail included, goes to --detail (default gpurun_out/bench_detail.json).
+roofline.on_chip also carries the clock measured under this load (profiles/<round>/clock_under_load.json,
+tools/clock_probe.sh).  DSE_BENCH_SET=key=value,... sets engine options on the sweep's context (A/Bs).
   partitioned    N = 2, 4, 8 only, after the timed sweep: config 5 with the N = 30 register split
                  over the N ranks (tools/bench_partitioned.py as a child process per rank, RCCL
                  index-swap all-to-all over xGMI): ms per H application, exchanged bytes per rank,
