@@ -166,7 +166,7 @@ def cpu_baseline(fraction: float, cores: int):
 
 
 WHT_PMC_N30 = next((q for q in (os.path.join(ROOT, "profiles", r, "wht_n30_pmc_traffic.json")
-                                 for r in ("r05", "r04", "r01")) if os.path.exists(q)),
+                                 for r in ("r06", "r05", "r04", "r01")) if os.path.exists(q)),
                    os.path.join(ROOT, "profiles", "r01", "wht_n30_pmc_traffic.json"))
 
 
@@ -180,9 +180,10 @@ def diag_energy(prob) -> float:
 def large_register(device: int, n_sea: int = 29):
     """Config 5 on one GPU (N = n_sea + 1 = 30, center_on, 50 kHz, t_final 5e-6 s, 6 outputs): the
     Walsh-Hadamard engine's H|psi> passes against the HBM roofline.  Bytes per amplitude and H
-    application are the passes' algorithmic traffic (FIRST 48, FWD/MID/INV 64 each, FINAL 80 + acc
-    32 every third term); "traffic" is the rocprofv3 FETCH/WRITE count of the same passes
-    (profiles/r01/wht_n30_pmc_traffic.json).  Kernel time per H application from HIP events
+    application are the passes' algorithmic traffic: FWD/MID/INV 64 each, FINAL 80 + acc 32 every
+    third term, and the next term's A and B (32) written by the same pass (option wht_fuse, the
+    default; FIRST's 48 once per interval, not counted); "traffic" is the rocprofv3 FETCH/WRITE count
+    of the same passes (profiles/<round>/wht_n30_pmc_traffic.json, tools/gpu.sh traffic_large).  Kernel time per H application from HIP events
     (excludes the first call's device allocation of 5 x 16 GiB).  "check": exact invariants of the
     unitary evolution on the 2^30 state (no reference state exists at this size): ||psi(t)|| = 1 at
     every output and <H> of the final state = <psi0|H|psi0> (dse_energy, on the device)."""
@@ -195,7 +196,7 @@ def large_register(device: int, n_sea: int = 29):
     n = prob.n_qubits
     wl = 13
     groups = 1 + -(-(n - wl) // (wl - 2))
-    bpa = 48.0 + 64.0 * (2 * groups - 3) + 80.0 + 32.0 / 3.0
+    bpa = 64.0 * (2 * groups - 3) + 80.0 + 32.0 / 3.0 + 32.0
     with Engine(device) as eng:
         pid = eng.add(prob)
         t0 = time.perf_counter()
@@ -218,16 +219,19 @@ def large_register(device: int, n_sea: int = 29):
         if n != 30:
             traffic_error = f"counter record is for N = 30, this register is N = {n}"
         else:
+            # MODE_GEN launches of FWD (1), MID (2), INV (3) (k_wht or the half-LDS k_wht_h) and of
+            # FINAL_NEXT (5, the fused default) or FIRST (0) + FINAL (4) in a record of the unfused passes
             per_pass = {}
             for name, rec in k.items():
-                m = re.fullmatch(r"k_wht<13, (\d), 2(?:, \d+)?>", name)
+                m = re.fullmatch(r"k_wht(?:_h)?<13, (\d), 2(?:, \d+)?>", name)
                 if m:
                     per_pass[int(m.group(1))] = per_pass.get(int(m.group(1)), 0.0) + rec["traffic_bytes_per_launch"]
-            missing = [ps for ps in range(5) if ps not in per_pass]
+            need = (1, 2, 3, 5) if 5 in per_pass else (0, 1, 2, 3, 4)
+            missing = [ps for ps in need if ps not in per_pass]
             if missing:
                 traffic_error = f"passes {missing} missing from {os.path.relpath(WHT_PMC_N30, ROOT)}"
             else:
-                traffic = sum(per_pass.values())
+                traffic = sum(per_pass[ps] for ps in need)
     except (OSError, KeyError, ValueError) as exc:
         traffic_error = f"counter record unreadable: {exc!r}"
     check = {"max_norm_error": float(np.max(np.abs(obs[0, 6] - 1.0))),
